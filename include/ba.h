@@ -1,0 +1,170 @@
+/*
+ * ba.h -- C ABI of libba_hip.so, the MI355X-native batched OM(m)
+ * Byzantine-agreement engine.
+ *
+ * The reference (mathiasplans/byzantine-agreement, /root/reference/ba.py) has no
+ * FFI: its hot path is a set of in-process Python methods that the REPL calls
+ * (ba.py:381 order, ba.py:386 wait_majority, ba.py:395 quorum, ba.py:399 clear)
+ * plus the rpyc service surface between generals (Serv.exposed_*, ba.py:25-63).
+ * Each entry point below names the reference interface it replaces.  The
+ * ctypes binding a maintainer adds on the reference side is in INTEGRATION.md.
+ *
+ * Conventions
+ *   - Every function returns 0 (BA_OK) or a negative BA_E* code; no exception
+ *     or C++ type crosses the ABI.  ba_last_error() gives a thread-local text.
+ *   - Host-pointer entry points copy in/out over PCIe; *_device entry points
+ *     take device pointers and a hipStream_t (as void*) and are asynchronous.
+ *   - One ctx per host thread; a ctx is not thread-safe.  The library owns
+ *     the device scratch it allocates inside the ctx.
+ *
+ * General indexing: the live generals sorted by id are
+ * indexed 0..n-1; index 0 is the commander (lowest live id, ba.py:381 +
+ * election ba.py:126-157); 1..n-1 are lieutenants.  n <= BA_MAX_GENERALS.
+ */
+#ifndef BA_H
+#define BA_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BA_ABI_VERSION 1
+#define BA_MAX_GENERALS 32
+#define BA_MAX_DEPTH 8
+#define BA_NCOUNTERS 16
+
+/* error codes */
+#define BA_OK 0
+#define BA_EINVAL (-1)     /* bad argument (n, m, modes, sizes, null pointer)   */
+#define BA_ENOMEM (-2)     /* device or host allocation failed                  */
+#define BA_EDEVICE (-3)    /* HIP runtime error / no device                     */
+#define BA_ENOTSUP (-4)    /* combination not supported (e.g. table mode, m>1)  */
+#define BA_ETOOBIG (-5)    /* tree too large for the requested engine          */
+
+/* lie source for faulty senders (ba.py:45, ba.py:269: random.randint(0,1)) */
+#define BA_LIE_PHILOX 0 /* Philox4x32-10 keyed by (seed; trial word, level, slot) */
+#define BA_LIE_TABLE 1  /* coins supplied in ba.py's canonical draw order (m=1)   */
+
+/* faulty-set source (ba.py:401-407 g-state <id> faulty) */
+#define BA_FAULTY_GIVEN 0  /* faulty_mask[] supplied by the caller               */
+#define BA_FAULTY_RANDOM 1 /* f ~ U{0..f}, uniform f-subset of the n generals    */
+#define BA_FAULTY_EXACT 2  /* exactly f faulty, uniform f-subset                 */
+
+/* commander order source (ba.py:367-381 actual-order <o>) */
+#define BA_ORDER_GIVEN 0  /* order[] supplied by the caller                     */
+#define BA_ORDER_RANDOM 1 /* Bernoulli(1/2) attack/retreat                      */
+#define BA_ORDER_CONST 2  /* every trial uses order_value                       */
+
+/* order / decision codes.  Any order other than "attack" is relayed as
+ * non-attack (ba.py:163-167, 177-181); the commander's own tally keeps it as
+ * "other" (ba.py:208-215). */
+#define BA_RETREAT 0
+#define BA_ATTACK 1
+#define BA_OTHER 2     /* order code only: e.g. `actual-order foo`           */
+#define BA_UNDEFINED 2 /* decision code: root tie (ba.py:194-195)            */
+
+/* quorum outcome codes (ba.py:246-253) */
+#define BA_Q_RETREAT 0
+#define BA_Q_ATTACK 1
+#define BA_Q_UNDETERMINED 2
+
+/* engines */
+#define BA_ENGINE_AUTO 0
+#define BA_ENGINE_FUSED 1  /* whole tree per 64-trial word resident on-chip     */
+#define BA_ENGINE_LEVELS 2 /* level-synchronous, bit-packed levels in HBM       */
+
+typedef struct ba_params {
+    uint32_t n;            /* live generals, 1..32                                */
+    uint32_t m;            /* OM depth; ba.py is m=1.  Effective depth min(m,n-2)   */
+    uint64_t seed;         /* Philox key for lies and synthetic inputs           */
+    uint32_t lie_mode;     /* BA_LIE_*                                            */
+    uint32_t faulty_mode;  /* BA_FAULTY_*                                         */
+    uint32_t f;            /* RANDOM: max f;  EXACT: f                            */
+    uint32_t order_mode;   /* BA_ORDER_*                                          */
+    uint32_t order_value;  /* BA_ORDER_CONST: BA_RETREAT/BA_ATTACK/BA_OTHER       */
+    uint32_t engine;       /* BA_ENGINE_*                                         */
+    uint64_t first_trial;  /* global index of trial 0; multiple of 64             */
+    uint32_t table_stride; /* BA_LIE_TABLE: uint32 words per trial in lie_table   */
+    uint32_t reserved[5];
+} ba_params;
+
+/* Run counters (integer sums; identical for any sharding of the trials). */
+#define BA_C_TRIALS 0          /* trials resolved                                   */
+#define BA_C_AGREEMENT 1       /* IC1: all loyal lieutenants decided alike          */
+#define BA_C_VALID_APPL 2      /* commander loyal (IC2 applicable)                   */
+#define BA_C_VALIDITY 3        /* IC2: loyal commander => loyal lts decide its order */
+#define BA_C_Q_RETREAT 4       /* quorum outcome counts (ba.py:246-253)              */
+#define BA_C_Q_ATTACK 5
+#define BA_C_Q_UNDETERMINED 6
+#define BA_C_UNDEF_DECISIONS 7 /* lieutenant decisions == undefined (root ties)      */
+#define BA_C_IN_BOUND 8        /* trials with f <= m_eff and n > 3 m_eff             */
+#define BA_C_BOUND_VIOL 9      /* in-bound trials violating IC1 or IC2               */
+#define BA_C_FAULTY_TOTAL 10   /* sum of f over trials                               */
+#define BA_C_ATTACK_DECISIONS 11 /* lieutenant decisions == attack                   */
+
+typedef struct ba_counters {
+    uint64_t v[BA_NCOUNTERS];
+} ba_counters;
+
+/* Per-trial outputs
+ *   decisions[t] : uint64, bits [2(r-1), 2(r-1)+1] = decision code of lieutenant r
+ *                  (BA_RETREAT / BA_ATTACK / BA_UNDEFINED), r = 1..n-1.
+ *                  Replaces Process.majority of each lieutenant (ba.py:188-195).
+ *   outcome[t]   : uint8, bits 0-1 quorum code (ba.py:225-255), bit 2 IC1,
+ *                  bit 3 IC2 applicable, bit 4 IC2, bit 5 in-bound.
+ * Per-trial inputs
+ *   faulty_mask[t] : uint32, bit i = general i faulty (ba.py:73, 407)
+ *   order[t]       : uint8 order code (ba.py:381 cmd[1])
+ *   lie_table      : table_stride uint32 words per trial; bit c (word c/32, bit
+ *                    c%32) is the c-th coin of ba.py's canonical draw order,
+ *                    1 = "attack" (random.randint(0,1) == 0).
+ *   poll_commander : uint32 per trial (BA_LIE_TABLE only, NULL = none): bit r set
+ *                    means lieutenant r also polls the commander in its relay
+ *                    round.  ba.py:171 skips only the port a lieutenant believes is
+ *                    the primary's; after g-add/g-kill that port can be stale or -1
+ *                    (ba.py:86-102, 114-115), so the commander's answer is counted
+ *                    too.  The stride must hold (n-1) + (n-1)^2 coins.
+ */
+
+/* ---- library / context (replaces Process/Serv lifecycle, ba.py:66-112) ---- */
+int ba_version(void);
+int ba_device_count(int* count);
+int ba_ctx_create(int device, struct ba_ctx** out);
+void ba_ctx_destroy(struct ba_ctx* ctx);
+const char* ba_last_error(void);
+
+/* ---- the hot path -------------------------------------------------------
+ * One call resolves `batch` independent OM(m) trials: commander send
+ * (Process.order, ba.py:257-285), the relay tree with the lie rule
+ * (Serv.exposed_get_order, ba.py:42-57), the recursive majority
+ * (Process.get_majority, ba.py:159-195) and the quorum epilogue
+ * (get_majorities + quorum, ba.py:197-255).  Null optional pointers:
+ * faulty_mask (unless BA_FAULTY_GIVEN), order (unless BA_ORDER_GIVEN),
+ * lie_table (unless BA_LIE_TABLE), decisions, outcome, counters.
+ * Counters are OVERWRITTEN with this call's totals.
+ */
+int ba_run_trials(struct ba_ctx* ctx, const ba_params* p, uint64_t batch,
+                  const uint32_t* faulty_mask, const uint8_t* order,
+                  const uint32_t* lie_table, const uint32_t* poll_commander,
+                  uint64_t* decisions, uint8_t* outcome, ba_counters* counters);
+
+/* Same computation on device buffers, enqueued on `stream` (hipStream_t, NULL =
+ * the ctx stream).  d_counters (BA_NCOUNTERS uint64 on device) is ACCUMULATED
+ * into, so repeated calls sum; zero it first for one call's totals. */
+int ba_run_trials_device(struct ba_ctx* ctx, const ba_params* p, uint64_t batch,
+                         const uint32_t* d_faulty_mask, const uint8_t* d_order,
+                         const uint32_t* d_lie_table, const uint32_t* d_poll_commander,
+                         uint64_t* d_decisions, uint8_t* d_outcome, uint64_t* d_counters,
+                         void* stream);
+
+/* Tree geometry helpers (host only, no device needed). */
+uint64_t ba_tree_slots(uint32_t n, uint32_t m);             /* sum_k |L_k|       */
+uint64_t ba_level_slots(uint32_t n, uint32_t m, uint32_t k); /* |L_k|=P(n-1,k+1) */
+int ba_engine_for(uint32_t n, uint32_t m);                  /* engine AUTO picks */
+
+#ifdef __cplusplus
+}
+#endif
+#endif
