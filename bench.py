@@ -1,0 +1,210 @@
+"""bench.py -- OM(m) trial-decisions/s on MI355X (BASELINE.json metric, config 2).
+
+A step resolves one batch of synthetic trials (n=10 generals, OM(3), 1M trials
+per GPU by default: faulty set = uniform f-subset with f ~ U{0..3}, order ~
+Bernoulli(1/2), lies from Philox -- all generated on the device from the seed,
+so the inputs are "resident" before the timed region by construction).  Each
+trial is fully resolved: every lieutenant's root decision is written to HBM
+(uint64/trial), plus the per-trial quorum/IC outcome byte, plus run counters.
+
+N>1: launched one process per GPU by torch.distributed.run.  Trials shard by
+global index (weak scaling, no data-path collective); the run counters are
+all-reduced once over RCCL at the end of the timed region.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md §Measurement for the roofline and
+cpu_baseline accounting.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "byzantine-agreement_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def algorithmic_bytes_per_trial(n: int, m: int) -> int:
+    """8 B per-trial I/O + 2 x ceil(bit-packed OM tree / 8)."""
+    from ba_amd import lib as L
+    slots = L.load().ba_tree_slots(n, m)
+    return 8 + 2 * ((slots + 7) // 8)
+
+
+def kernel_bytes(name: str, n: int, m: int, batch: int) -> int:
+    """Algorithmic HBM bytes of one launch of `name` over `batch` trials."""
+    from ba_amd import lib as L
+    lib = L.load()
+    me = L.effective_depth(n, m)
+    S = [lib.ba_level_slots(n, m, k) for k in range(me + 1)]
+    words = (batch + 63) // 64
+    if name == "k_relay_leaf":  # write L_me once, read L_{me-1} once
+        return 8 * words * (S[me] + S[me - 1])
+    if name == "k_majority_leaf":  # read L_me + L_{me-1}, write R_{me-1}
+        return 8 * words * (S[me] + 2 * S[me - 1])
+    if name.startswith("k_fused"):
+        return algorithmic_bytes_per_trial(n, m) * batch
+    return 0
+
+
+def run_cpu_baseline(n, m, seed, fmax, budget_s):
+    """Time the C oracle (oracle/ba_oracle.c, OpenMP) on a bounded sample of the
+    same synthetic workload (same seed, first trials of the stream)."""
+    import oracle_c
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    kw = dict(seed=seed, faulty_mode=1, f=fmax, order_mode=1)
+    probe = 64 * threads
+    t0 = time.perf_counter()
+    oracle_c.run(n, m, probe, threads=threads, **kw)
+    dt = time.perf_counter() - t0
+    rate = probe / max(dt, 1e-9)
+    sample = int(min(max(rate * budget_s, probe), 1 << 22)) // 64 * 64
+    t0 = time.perf_counter()
+    oracle_c.run(n, m, sample, threads=threads, **kw)
+    dt = time.perf_counter() - t0
+    return {"value": sample / dt, "unit": "trial-decisions/s", "cores": threads, "kind": "port",
+            "sample": f"C oracle (oracle/ba_oracle.c, OpenMP x{threads}) on the first {sample} "
+                      f"trials of the same n={n}, m={m} synthetic stream, {dt:.1f} s; "
+                      f"host CPU: {cpu_model()}, nproc={os.cpu_count()}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=10)
+    ap.add_argument("--m", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1 << 20, help="trials per GPU per step")
+    ap.add_argument("--fmax", type=int, default=-1)
+    ap.add_argument("--seed", type=lambda s: int(s, 0), default=0xBA5EED)
+    ap.add_argument("--engine", default="auto", choices=["auto", "fused", "levels"])
+    ap.add_argument("--cpu-budget-s", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    from ba_amd import lib as L
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+    n, m, B = args.n, args.m, args.batch
+    fmax = L.default_fmax(n) if args.fmax < 0 else args.fmax
+    engine_id = {"auto": L.ENGINE_AUTO, "fused": L.ENGINE_FUSED, "levels": L.ENGINE_LEVELS}[args.engine]
+    eng = L.Engine(dev.index)
+    dec = torch.empty(B, dtype=torch.int64, device=dev)
+    out = torch.empty(B, dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(16, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(i):
+        first = (i * world + rank) * B  # global trial index: weak scaling, disjoint shards
+        p = L.make_params(n, m, args.seed, L.LIE_PHILOX, L.FAULTY_RANDOM, fmax, L.ORDER_RANDOM,
+                          L.ATTACK, engine_id, first)
+        eng.run_device(p, B, d_decisions=dec.data_ptr(), d_outcome=out.data_ptr(),
+                       d_counters=cnt.data_ptr(), stream=stream.cuda_stream)
+
+    for i in range(args.warmup):
+        step(i)
+    cnt.zero_()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for i in range(args.steps):
+        step(args.warmup + i)
+    if dist:
+        dist.all_reduce(cnt)  # the only collective: run counters (RCCL)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    elapsed = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    T = float(elapsed.item())
+    gpu_ms = ev0.elapsed_time(ev1)
+    counters = dict(zip(L.COUNTER_NAMES, [int(x) for x in cnt.cpu().tolist()]))
+    total_trials = B * args.steps * world
+    value = total_trials / T
+
+    # per-kernel HIP-event timing on the launch stream (a second pass of the same steps)
+    kernels, roof = {}, None
+    if not args.no_profile:
+        eng.profile(True)
+        for i in range(args.steps):
+            step(args.warmup + args.steps + i)
+        torch.cuda.synchronize(dev)
+        kernels = eng.profile_read()
+        eng.profile(False)
+        if kernels:
+            name, (nl, ms) = max(kernels.items(), key=lambda kv: kv[1][1])
+            avg_ms = ms / nl
+            alg = kernel_bytes(name, n, m, B)
+            achieved = alg / (avg_ms * 1e-3) / 1e9 if alg else None
+            roof = {"bound": "hbm", "kernel": name, "avg_ms": round(avg_ms, 4),
+                    "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                    "traffic": None, "algorithmic_bytes_per_launch": alg}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = run_cpu_baseline(n, m, args.seed, fmax, args.cpu_budget_s)
+
+    if rank == 0:
+        line = {
+            "metric": "OM(m) trial-decisions/sec (whole node) at n=10,m=3; achieved HBM GB/s",
+            "value": round(value, 1), "unit": "trial-decisions/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(T * 1e3 / args.steps, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic (Philox-generated faulty sets, orders and lies on device)",
+            "config": {"workload": f"OM({m}) n={n}, {B} trials/GPU/step, f~U{{0..{fmax}}}, "
+                                   f"random order, decisions+outcome written",
+                       "n": n, "m": m, "trials_per_gpu_step": B, "engine": args.engine,
+                       "parallelism": f"trial-dp{world}"},
+            "gpu_event_ms": round(gpu_ms, 3),
+            "kernels_ms": {k: round(v[1] / v[0], 4) for k, v in kernels.items()},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "counters": counters,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,218 @@
+"""ctypes binding of libba_hip.so (include/ba.h).
+
+This is the only way the Python side reaches the hot path.  There is no CPU
+fallback: if the shared library is missing, or no HIP device is visible, the
+calls raise.  The oracle under /oracle is test infrastructure and is never
+imported here.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("BA_HIP_LIB", os.path.join(HERE, "libba_hip.so"))
+
+# numeric contract of include/ba.h
+ABI_VERSION = 1
+MAX_GENERALS = 32
+MAX_DEPTH = 8
+NCOUNTERS = 16
+OK, EINVAL, ENOMEM, EDEVICE, ENOTSUP, ETOOBIG = 0, -1, -2, -3, -4, -5
+LIE_PHILOX, LIE_TABLE = 0, 1
+FAULTY_GIVEN, FAULTY_RANDOM, FAULTY_EXACT = 0, 1, 2
+ORDER_GIVEN, ORDER_RANDOM, ORDER_CONST = 0, 1, 2
+RETREAT, ATTACK, OTHER, UNDEFINED = 0, 1, 2, 2
+Q_RETREAT, Q_ATTACK, Q_UNDETERMINED = 0, 1, 2
+ENGINE_AUTO, ENGINE_FUSED, ENGINE_LEVELS = 0, 1, 2
+COUNTER_NAMES = ["trials", "agreement", "validity_applicable", "validity", "quorum_retreat",
+                 "quorum_attack", "quorum_undetermined", "undefined_decisions", "in_bound",
+                 "bound_violations", "faulty_total", "attack_decisions"]
+EXPORTS = ["ba_version", "ba_device_count", "ba_ctx_create", "ba_ctx_destroy", "ba_last_error",
+           "ba_run_trials", "ba_run_trials_device", "ba_tree_slots", "ba_level_slots",
+           "ba_engine_for", "ba_profile_enable", "ba_profile_read"]
+
+
+class BAError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libba_hip error {code}: {msg}")
+        self.code = code
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint32), ("m", ctypes.c_uint32), ("seed", ctypes.c_uint64),
+                ("lie_mode", ctypes.c_uint32), ("faulty_mode", ctypes.c_uint32),
+                ("f", ctypes.c_uint32), ("order_mode", ctypes.c_uint32),
+                ("order_value", ctypes.c_uint32), ("engine", ctypes.c_uint32),
+                ("first_trial", ctypes.c_uint64), ("table_stride", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32 * 5)]
+
+
+class Counters(ctypes.Structure):
+    _fields_ = [("v", ctypes.c_uint64 * NCOUNTERS)]
+
+
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load libba_hip.so (raises if it is absent: there is no fallback)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise FileNotFoundError(f"{p} not built: run `make -C byzantine-agreement_amd` "
+                                f"or __graft_entry__.build()")
+    lib = ctypes.CDLL(p)
+    vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    lib.ba_version.restype = i32
+    lib.ba_device_count.argtypes = [ctypes.POINTER(i32)]
+    lib.ba_ctx_create.argtypes = [i32, ctypes.POINTER(vp)]
+    lib.ba_ctx_destroy.argtypes = [vp]
+    lib.ba_ctx_destroy.restype = None
+    lib.ba_last_error.restype = ctypes.c_char_p
+    lib.ba_run_trials.argtypes = [vp, ctypes.POINTER(Params), u64, vp, vp, vp, vp, vp, vp,
+                                  ctypes.POINTER(Counters)]
+    lib.ba_run_trials_device.argtypes = [vp, ctypes.POINTER(Params), u64, vp, vp, vp, vp, vp,
+                                         vp, vp, vp]
+    lib.ba_tree_slots.argtypes = [u32, u32]
+    lib.ba_tree_slots.restype = u64
+    lib.ba_level_slots.argtypes = [u32, u32, u32]
+    lib.ba_level_slots.restype = u64
+    lib.ba_engine_for.argtypes = [u32, u32]
+    lib.ba_profile_enable.argtypes = [vp, i32]
+    lib.ba_profile_read.argtypes = [vp, i32, ctypes.c_char_p, i32, ctypes.POINTER(u64),
+                                    ctypes.POINTER(ctypes.c_double)]
+    if lib.ba_version() != ABI_VERSION:
+        raise RuntimeError(f"libba_hip ABI {lib.ba_version()} != {ABI_VERSION}")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _check(lib, rc: int):
+    if rc != OK:
+        raise BAError(rc, lib.ba_last_error().decode())
+
+
+def effective_depth(n: int, m: int) -> int:
+    return min(m, n - 2) if n >= 2 else 0
+
+
+def default_fmax(n: int) -> int:
+    """f ~ U{0..floor((n-1)/3)} for random-set configs."""
+    return (n - 1) // 3
+
+
+def table_stride(n: int) -> int:
+    """uint32 words per trial a ba.py draw-order table needs: (n-1) + (n-1)^2 coins."""
+    L = n - 1
+    return max(1, (L + L * L + 31) // 32)
+
+
+@dataclass
+class RunResult:
+    decisions: np.ndarray | None
+    outcome: np.ndarray | None
+    counters: dict = field(default_factory=dict)
+
+    def decision(self, t: int, r: int) -> int:
+        """Decision code of lieutenant r (1..n-1) in trial t."""
+        return int((int(self.decisions[t]) >> (2 * (r - 1))) & 3)
+
+
+def make_params(n, m, seed=0, lie_mode=LIE_PHILOX, faulty_mode=FAULTY_GIVEN, f=0,
+                order_mode=ORDER_GIVEN, order_value=ATTACK, engine=ENGINE_AUTO,
+                first_trial=0, stride=0) -> Params:
+    p = Params()
+    p.n, p.m, p.seed = n, m, seed & ((1 << 64) - 1)
+    p.lie_mode, p.faulty_mode, p.f = lie_mode, faulty_mode, f
+    p.order_mode, p.order_value, p.engine = order_mode, order_value, engine
+    p.first_trial, p.table_stride = first_trial, stride
+    return p
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+class Engine:
+    """One libba_hip context on one HIP device (mirrors a ba.py process group)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        h = ctypes.c_void_p()
+        _check(self.lib, self.lib.ba_ctx_create(device, ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            self.lib.ba_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def run(self, n, m, batch, seed=0, lie_mode=LIE_PHILOX, faulty_mode=FAULTY_GIVEN, f=0,
+            order_mode=ORDER_GIVEN, order_value=ATTACK, engine=ENGINE_AUTO, first_trial=0,
+            faulty=None, order=None, table=None, poll=None, want_decisions=True,
+            want_outcome=True) -> RunResult:
+        """Resolve `batch` trials through host buffers (PCIe copies included)."""
+        faulty = None if faulty is None else np.ascontiguousarray(faulty, dtype=np.uint32)
+        order = None if order is None else np.ascontiguousarray(order, dtype=np.uint8)
+        stride = 0
+        if table is not None:
+            table = np.ascontiguousarray(table, dtype=np.uint32)
+            stride = table.shape[1]
+        poll = None if poll is None else np.ascontiguousarray(poll, dtype=np.uint32)
+        dec = np.zeros(batch, np.uint64) if want_decisions else None
+        out = np.zeros(batch, np.uint8) if want_outcome else None
+        p = make_params(n, m, seed, lie_mode, faulty_mode, f, order_mode, order_value, engine,
+                        first_trial, stride)
+        cnt = Counters()
+        _check(self.lib, self.lib.ba_run_trials(self.handle, ctypes.byref(p), batch, _ptr(faulty),
+                                                _ptr(order), _ptr(table), _ptr(poll), _ptr(dec),
+                                                _ptr(out), ctypes.byref(cnt)))
+        return RunResult(dec, out, dict(zip(COUNTER_NAMES, [int(x) for x in cnt.v])))
+
+    def profile(self, on: bool):
+        """Enable/disable per-kernel HIP-event timing (clears the totals)."""
+        _check(self.lib, self.lib.ba_profile_enable(self.handle, int(on)))
+
+    def profile_read(self) -> dict:
+        """{kernel name: (launches, total ms)} since profiling was enabled."""
+        out, i = {}, 0
+        name = ctypes.create_string_buffer(64)
+        n = ctypes.c_uint64()
+        ms = ctypes.c_double()
+        while self.lib.ba_profile_read(self.handle, i, name, 64, ctypes.byref(n), ctypes.byref(ms)) == OK:
+            out[name.value.decode()] = (int(n.value), float(ms.value))
+            i += 1
+        return out
+
+    def run_device(self, params: Params, batch: int, d_faulty=0, d_order=0, d_table=0, d_poll=0,
+                   d_decisions=0, d_outcome=0, d_counters=0, stream=0):
+        """Enqueue on device pointers (ints, e.g. torch tensor .data_ptr()); asynchronous."""
+        _check(self.lib, self.lib.ba_run_trials_device(
+            self.handle, ctypes.byref(params), batch, d_faulty or None, d_order or None,
+            d_table or None, d_poll or None, d_decisions or None, d_outcome or None,
+            d_counters or None, stream or None))
+
+
+def pack_coins(rows, n):
+    """Pack per-trial coin lists (1 = attack) into a (batch, stride) uint32 table."""
+    stride = table_stride(n)
+    tab = np.zeros((len(rows), stride), np.uint32)
+    for i, coins in enumerate(rows):
+        for c, v in enumerate(coins):
+            if v:
+                tab[i, c >> 5] |= np.uint32(1 << (c & 31))
+    return tab

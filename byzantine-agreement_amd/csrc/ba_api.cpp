@@ -1,0 +1,470 @@
+// ba_api.cpp -- the C ABI of libba_hip.so (include/ba.h).
+//
+// Validation, context/device-memory ownership, engine selection and chunking
+// live here; the arithmetic lives in the HIP engines.  There is no CPU compute
+// path: without a HIP device every entry point fails with BA_EDEVICE.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+
+#include "../../include/ba.h"
+#include "ba_engine.hpp"
+
+using namespace ba;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                 \
+    do {                                                                              \
+        hipError_t _e = (expr);                                                       \
+        if (_e != hipSuccess)                                                         \
+            return fail(BA_EDEVICE, "%s failed: %s", #expr, hipGetErrorString(_e));   \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// geometry
+// ---------------------------------------------------------------------------
+static uint64_t perm_count(uint32_t L, uint32_t len) {
+    uint64_t p = 1;
+    for (uint32_t i = 0; i < len; ++i) {
+        if (L < i + 1) return 0;
+        p *= (uint64_t)(L - i);
+        if (p > (1ull << 40)) return 1ull << 40;  // saturate: far beyond any engine
+    }
+    return p;
+}
+
+static uint32_t effective_depth(uint32_t n, uint32_t m) {
+    if (n < 2) return 0;
+    return m < n - 2 ? m : n - 2;
+}
+
+namespace ba {
+bool Geometry::build(uint32_t n_, uint32_t me_, uint64_t max_level_slots) {
+    n = n_;
+    L = n_ - 1;
+    me = me_;
+    S.assign(me + 1, 0);
+    slots_total = inner_total = 0;
+    for (uint32_t k = 0; k <= me; ++k) {
+        S[k] = perm_count(L, k + 1);
+        if (S[k] > max_level_slots) return false;
+        slots_total += S[k];
+        if (k >= 1 && k < me) inner_total += S[k];
+    }
+    // sender table: general index of the last relayer of every slot at levels
+    // 0..me-1 (lexicographic DFS visits each level's slots in rank order).
+    sender_off.assign(me, 0);
+    uint64_t off = 0;
+    for (uint32_t k = 0; k < me; ++k) {
+        sender_off[k] = off;
+        off += S[k];
+    }
+    sender.assign(off, 0);
+    std::vector<uint64_t> fill(me, 0);
+    // iterative DFS over relay paths of length 1..me in lexicographic order
+    std::vector<uint32_t> next(me + 1, 0);
+    std::vector<uint32_t> usedv(me + 1, 0);
+    if (me > 0) {
+        uint32_t depth = 0;
+        usedv[0] = 0;
+        next[0] = 0;
+        while (true) {
+            // find next candidate at this depth
+            uint32_t c = next[depth];
+            while (c < L && ((usedv[depth] >> c) & 1u)) ++c;
+            if (c >= L) {
+                if (depth == 0) break;
+                --depth;
+                continue;
+            }
+            next[depth] = c + 1;
+            // path of length depth+1 ending in c -> slot of level `depth`
+            sender[sender_off[depth] + fill[depth]++] = (uint8_t)(c + 1);
+            if (depth + 1 < me) {
+                usedv[depth + 1] = usedv[depth] | (1u << c);
+                next[depth + 1] = 0;
+                ++depth;
+            }
+        }
+    }
+    return true;
+}
+
+void LevelsLayout::plan(const Geometry& g, uint64_t W_) {
+    W = W_;
+    uint64_t o = 0;
+    F = o; o += (uint64_t)g.n * W;
+    OB = o; o += W;
+    OO = o; o += W;
+    VAL = o; o += W;
+    Lk.assign(g.me + 1, 0);
+    for (uint32_t k = 0; k <= g.me; ++k) { Lk[k] = o; o += g.S[k] * W; }
+    Rp.assign(g.me + 1, 0);
+    for (uint32_t p = 1; p < g.me; ++p) { Rp[p] = o; o += g.S[p] * W; }
+    total = o;
+}
+}  // namespace ba
+
+// ---------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int grow(size_t need) {
+        if (need <= bytes) return BA_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        if (need == 0) return BA_OK;
+        hipError_t e = hipMalloc(&p, need);
+        if (e != hipSuccess)
+            return fail(BA_ENOMEM, "hipMalloc(%zu) failed: %s", need, hipGetErrorString(e));
+        bytes = need;
+        return BA_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+struct GeoEntry {
+    Geometry g;
+    DevBuf sender;
+};
+
+struct ProfTotal {
+    uint64_t launches = 0;
+    double ms = 0.0;
+};
+
+struct ba_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    size_t scratch_budget = 8ull << 30;
+    DevBuf scratch, partials, io_faulty, io_order, io_table, io_poll, io_dec, io_out, io_cnt;
+    std::map<uint64_t, std::unique_ptr<GeoEntry>> geos;
+    Prof prof;
+    std::map<std::string, ProfTotal> prof_totals;
+};
+
+namespace ba {
+hipEvent_t Prof::take() {
+    if (!pool.empty()) {
+        hipEvent_t e = pool.back();
+        pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+void Prof::begin(const char* name, hipStream_t s) {
+    stream = s;
+    Rec r{name, take(), take()};
+    (void)hipEventRecord(r.a, s);
+    pending.push_back(r);
+}
+void Prof::end() { (void)hipEventRecord(pending.back().b, stream); }
+}  // namespace ba
+
+// Drain recorded events into per-kernel totals (synchronises on the events).
+static void prof_collect(ba_ctx* ctx) {
+    for (auto& r : ctx->prof.pending) {
+        (void)hipEventSynchronize(r.b);
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+            ProfTotal& t = ctx->prof_totals[r.name];
+            t.launches += 1;
+            t.ms += ms;
+        }
+        ctx->prof.pool.push_back(r.a);
+        ctx->prof.pool.push_back(r.b);
+    }
+    ctx->prof.pending.clear();
+}
+
+extern "C" int ba_profile_enable(ba_ctx* ctx, int on) {
+    if (!ctx) return fail(BA_EINVAL, "ctx is NULL");
+    prof_collect(ctx);
+    ctx->prof_totals.clear();
+    ctx->prof.on = on != 0;
+    return BA_OK;
+}
+
+extern "C" int ba_profile_read(ba_ctx* ctx, int index, char* name, int name_len,
+                               uint64_t* launches, double* total_ms) {
+    if (!ctx) return fail(BA_EINVAL, "ctx is NULL");
+    prof_collect(ctx);
+    if (index < 0 || index >= (int)ctx->prof_totals.size())
+        return fail(BA_EINVAL, "profile index %d out of range", index);
+    auto it = ctx->prof_totals.begin();
+    std::advance(it, index);
+    if (name && name_len > 0) snprintf(name, (size_t)name_len, "%s", it->first.c_str());
+    if (launches) *launches = it->second.launches;
+    if (total_ms) *total_ms = it->second.ms;
+    return BA_OK;
+}
+
+extern "C" int ba_version(void) { return BA_ABI_VERSION; }
+
+extern "C" const char* ba_last_error(void) { return g_err.c_str(); }
+
+extern "C" int ba_device_count(int* count) {
+    if (!count) return fail(BA_EINVAL, "count is NULL");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) {
+        *count = 0;
+        return fail(BA_EDEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    }
+    *count = c;
+    return BA_OK;
+}
+
+extern "C" int ba_ctx_create(int device, ba_ctx** out) {
+    if (!out) return fail(BA_EINVAL, "out is NULL");
+    *out = nullptr;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess || c == 0)
+        return fail(BA_EDEVICE, "no HIP device visible (libba_hip has no CPU path)");
+    if (device < 0 || device >= c) return fail(BA_EINVAL, "device %d out of range [0,%d)", device, c);
+    HIP_TRY(hipSetDevice(device));
+    auto* ctx = new ba_ctx();
+    ctx->device = device;
+    if (const char* s = getenv("BA_SCRATCH_BYTES")) ctx->scratch_budget = strtoull(s, nullptr, 0);
+    hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete ctx;
+        return fail(BA_EDEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    *out = ctx;
+    return BA_OK;
+}
+
+extern "C" void ba_ctx_destroy(ba_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    prof_collect(ctx);
+    for (hipEvent_t e : ctx->prof.pool) (void)hipEventDestroy(e);
+    for (DevBuf* b : {&ctx->scratch, &ctx->partials, &ctx->io_faulty, &ctx->io_order, &ctx->io_table,
+                      &ctx->io_poll, &ctx->io_dec, &ctx->io_out, &ctx->io_cnt})
+        b->release();
+    for (auto& kv : ctx->geos) kv.second->sender.release();
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+extern "C" uint64_t ba_level_slots(uint32_t n, uint32_t m, uint32_t k) {
+    if (n < 1 || n > BA_MAX_GENERALS) return 0;
+    if (k > effective_depth(n, m)) return 0;
+    return perm_count(n - 1, k + 1);
+}
+
+extern "C" uint64_t ba_tree_slots(uint32_t n, uint32_t m) {
+    if (n < 1 || n > BA_MAX_GENERALS) return 0;
+    uint64_t s = 0;
+    const uint32_t me = effective_depth(n, m);
+    for (uint32_t k = 0; k <= me; ++k) s += perm_count(n - 1, k + 1);
+    return s;
+}
+
+extern "C" int ba_engine_for(uint32_t n, uint32_t m) {
+    (void)n;
+    (void)m;
+    return BA_ENGINE_LEVELS;
+}
+
+// ---------------------------------------------------------------------------
+// validation
+// ---------------------------------------------------------------------------
+static int validate(const ba_params* p, uint64_t batch, bool has_faulty, bool has_order,
+                    bool has_table) {
+    if (!p) return fail(BA_EINVAL, "params is NULL");
+    if (p->n < 1 || p->n > BA_MAX_GENERALS) return fail(BA_EINVAL, "n=%u outside [1,%d]", p->n, BA_MAX_GENERALS);
+    if (p->m > BA_MAX_DEPTH) return fail(BA_EINVAL, "m=%u > %d", p->m, BA_MAX_DEPTH);
+    if (p->lie_mode > BA_LIE_TABLE) return fail(BA_EINVAL, "lie_mode=%u", p->lie_mode);
+    if (p->faulty_mode > BA_FAULTY_EXACT) return fail(BA_EINVAL, "faulty_mode=%u", p->faulty_mode);
+    if (p->order_mode > BA_ORDER_CONST) return fail(BA_EINVAL, "order_mode=%u", p->order_mode);
+    if (p->order_mode == BA_ORDER_CONST && p->order_value > BA_OTHER)
+        return fail(BA_EINVAL, "order_value=%u", p->order_value);
+    if (p->faulty_mode == BA_FAULTY_EXACT && p->f > p->n)
+        return fail(BA_EINVAL, "exact f=%u > n=%u", p->f, p->n);
+    if (p->engine > BA_ENGINE_LEVELS) return fail(BA_EINVAL, "engine=%u", p->engine);
+    if (p->first_trial & 63) return fail(BA_EINVAL, "first_trial must be a multiple of 64");
+    if (batch && p->faulty_mode == BA_FAULTY_GIVEN && !has_faulty)
+        return fail(BA_EINVAL, "BA_FAULTY_GIVEN needs faulty_mask");
+    if (batch && p->order_mode == BA_ORDER_GIVEN && !has_order)
+        return fail(BA_EINVAL, "BA_ORDER_GIVEN needs order");
+    if (p->lie_mode == BA_LIE_TABLE) {
+        if (effective_depth(p->n, p->m) > 1)
+            return fail(BA_ENOTSUP, "table (ba.py draw-order) mode exists for OM(1) only");
+        const uint64_t L = p->n - 1, coins = L + L * L;
+        if ((uint64_t)p->table_stride * 32 < coins)
+            return fail(BA_EINVAL, "table_stride=%u words < %llu coins", p->table_stride,
+                        (unsigned long long)coins);
+        if (batch && !has_table) return fail(BA_EINVAL, "BA_LIE_TABLE needs lie_table");
+    }
+    return BA_OK;
+}
+
+static GeoEntry* geometry(ba_ctx* ctx, uint32_t n, uint32_t me, int* rc) {
+    const uint64_t key = (uint64_t)n << 8 | me;
+    auto it = ctx->geos.find(key);
+    if (it != ctx->geos.end()) return it->second.get();
+    auto ge = std::make_unique<GeoEntry>();
+    if (!ge->g.build(n, me, 1ull << 31)) {
+        *rc = fail(BA_ETOOBIG, "OM(%u) tree over %u generals has a level above 2^31 slots", me, n);
+        return nullptr;
+    }
+    if (!ge->g.sender.empty()) {
+        if ((*rc = ge->sender.grow(ge->g.sender.size())) != BA_OK) return nullptr;
+        hipError_t e = hipMemcpy(ge->sender.p, ge->g.sender.data(), ge->g.sender.size(),
+                                 hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            *rc = fail(BA_EDEVICE, "sender upload: %s", hipGetErrorString(e));
+            return nullptr;
+        }
+    }
+    GeoEntry* raw = ge.get();
+    ctx->geos.emplace(key, std::move(ge));
+    return raw;
+}
+
+// ---------------------------------------------------------------------------
+// device entry point
+// ---------------------------------------------------------------------------
+extern "C" int ba_run_trials_device(ba_ctx* ctx, const ba_params* p, uint64_t batch,
+                                    const uint32_t* d_faulty, const uint8_t* d_order,
+                                    const uint32_t* d_table, const uint32_t* d_poll,
+                                    uint64_t* d_decisions, uint8_t* d_outcome,
+                                    uint64_t* d_counters, void* stream) {
+    if (!ctx) return fail(BA_EINVAL, "ctx is NULL");
+    int rc = validate(p, batch, d_faulty != nullptr, d_order != nullptr, d_table != nullptr);
+    if (rc != BA_OK) return rc;
+    if (!d_counters) return fail(BA_EINVAL, "d_counters is required on the device path");
+    if (batch == 0) return BA_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+
+    RunArgs a;
+    a.n = p->n;
+    a.m = p->m;
+    a.me = effective_depth(p->n, p->m);
+    a.seed = p->seed;
+    a.lie_mode = p->lie_mode;
+    a.gen = GenSpec{p->faulty_mode, p->f, p->order_mode, p->order_value};
+    a.first_trial = p->first_trial;
+    a.table_stride = p->table_stride;
+    a.batch = batch;
+    a.faulty = p->faulty_mode == BA_FAULTY_GIVEN ? d_faulty : nullptr;
+    a.order = p->order_mode == BA_ORDER_GIVEN ? d_order : nullptr;
+    a.table = d_table;
+    a.poll = d_poll;
+    a.decisions = d_decisions;
+    a.outcome = d_outcome;
+    a.counters = d_counters;
+    a.stream = stream ? (hipStream_t)stream : ctx->stream;
+    a.prof = &ctx->prof;
+
+    if ((rc = ctx->partials.grow(sizeof(uint64_t) * 16 * kPartialRows)) != BA_OK) return rc;
+    uint64_t* partials = (uint64_t*)ctx->partials.p;
+
+    if (p->lie_mode == BA_LIE_TABLE) {
+        HIP_TRY(launch_table(a, partials));
+        return BA_OK;
+    }
+
+    GeoEntry* ge = geometry(ctx, a.n, a.me, &rc);
+    if (!ge) return rc;
+    const Geometry& g = ge->g;
+    // chunk the batch so the scratch fits the budget and 32-bit indices hold
+    const uint64_t per_word = LevelsLayout::words_per_trial_word(g) * sizeof(uint64_t);
+    uint64_t max_level = 0;
+    for (uint64_t s : g.S) max_level = s > max_level ? s : max_level;
+    uint64_t words = (batch + 63) / 64;
+    uint64_t chunk = ctx->scratch_budget / per_word;
+    const uint64_t idx_cap = (1ull << 31) / (max_level + 1);
+    if (chunk > idx_cap) chunk = idx_cap;
+    if (chunk > words) chunk = words;
+    if (chunk == 0)
+        return fail(BA_ETOOBIG, "one 64-trial word needs %llu bytes of scratch (budget %zu)",
+                    (unsigned long long)per_word, ctx->scratch_budget);
+    LevelsLayout lay;
+    lay.plan(g, chunk);
+    if ((rc = ctx->scratch.grow(lay.total * sizeof(uint64_t))) != BA_OK) return rc;
+    for (uint64_t w0 = 0; w0 < words; w0 += chunk) {
+        const uint64_t wn = (words - w0) < chunk ? (words - w0) : chunk;
+        const uint64_t trial0 = w0 * 64;
+        const uint64_t nt = (batch - trial0) < wn * 64 ? (batch - trial0) : wn * 64;
+        LevelsLayout cl;
+        cl.plan(g, wn);
+        HIP_TRY(launch_levels_chunk(a, g, (const uint8_t*)ge->sender.p, (uint64_t*)ctx->scratch.p,
+                                    cl, trial0, nt, partials));
+    }
+    return BA_OK;
+}
+
+// ---------------------------------------------------------------------------
+// host entry point: copy in, run, copy out (PCIe-inclusive)
+// ---------------------------------------------------------------------------
+extern "C" int ba_run_trials(ba_ctx* ctx, const ba_params* p, uint64_t batch,
+                             const uint32_t* faulty, const uint8_t* order,
+                             const uint32_t* lie_table, const uint32_t* poll,
+                             uint64_t* decisions, uint8_t* outcome, ba_counters* counters) {
+    if (!ctx) return fail(BA_EINVAL, "ctx is NULL");
+    int rc = validate(p, batch, faulty != nullptr, order != nullptr, lie_table != nullptr);
+    if (rc != BA_OK) return rc;
+    if (counters) memset(counters, 0, sizeof *counters);
+    if (batch == 0) return BA_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const bool need_f = p->faulty_mode == BA_FAULTY_GIVEN, need_o = p->order_mode == BA_ORDER_GIVEN;
+    const bool need_t = p->lie_mode == BA_LIE_TABLE, need_p = need_t && poll;
+    if (need_f && (rc = ctx->io_faulty.grow(batch * 4)) != BA_OK) return rc;
+    if (need_o && (rc = ctx->io_order.grow(batch)) != BA_OK) return rc;
+    if (need_t && (rc = ctx->io_table.grow(batch * p->table_stride * 4)) != BA_OK) return rc;
+    if (need_p && (rc = ctx->io_poll.grow(batch * 4)) != BA_OK) return rc;
+    if (decisions && (rc = ctx->io_dec.grow(batch * 8)) != BA_OK) return rc;
+    if (outcome && (rc = ctx->io_out.grow(batch)) != BA_OK) return rc;
+    if ((rc = ctx->io_cnt.grow(BA_NCOUNTERS * 8)) != BA_OK) return rc;
+    if (need_f) HIP_TRY(hipMemcpyAsync(ctx->io_faulty.p, faulty, batch * 4, hipMemcpyHostToDevice, st));
+    if (need_o) HIP_TRY(hipMemcpyAsync(ctx->io_order.p, order, batch, hipMemcpyHostToDevice, st));
+    if (need_t)
+        HIP_TRY(hipMemcpyAsync(ctx->io_table.p, lie_table, batch * p->table_stride * 4,
+                               hipMemcpyHostToDevice, st));
+    if (need_p) HIP_TRY(hipMemcpyAsync(ctx->io_poll.p, poll, batch * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(ctx->io_cnt.p, 0, BA_NCOUNTERS * 8, st));
+    rc = ba_run_trials_device(ctx, p, batch, need_f ? (const uint32_t*)ctx->io_faulty.p : nullptr,
+                              need_o ? (const uint8_t*)ctx->io_order.p : nullptr,
+                              need_t ? (const uint32_t*)ctx->io_table.p : nullptr,
+                              need_p ? (const uint32_t*)ctx->io_poll.p : nullptr,
+                              decisions ? (uint64_t*)ctx->io_dec.p : nullptr,
+                              outcome ? (uint8_t*)ctx->io_out.p : nullptr, (uint64_t*)ctx->io_cnt.p,
+                              st);
+    if (rc != BA_OK) return rc;
+    if (decisions) HIP_TRY(hipMemcpyAsync(decisions, ctx->io_dec.p, batch * 8, hipMemcpyDeviceToHost, st));
+    if (outcome) HIP_TRY(hipMemcpyAsync(outcome, ctx->io_out.p, batch, hipMemcpyDeviceToHost, st));
+    if (counters) HIP_TRY(hipMemcpyAsync(counters->v, ctx->io_cnt.p, BA_NCOUNTERS * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return BA_OK;
+}

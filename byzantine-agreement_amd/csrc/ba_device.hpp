@@ -1,0 +1,253 @@
+// ba_device.hpp -- device building blocks shared by the OM(m) engines (gfx950).
+//
+// Data model: one 64-bit word holds one tree slot for 64 consecutive trials
+// (bit b = trial 64*w + b), the natural product of a wave64 __ballot.  Relay
+// is a per-word bit-select, majorities are bit-sliced counters over words, and
+// a single Philox4x32-10 call yields the lie bits of two slots x 64 trials.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ba {
+
+constexpr int kMaxN = 32;
+constexpr uint32_t kGenTag = 0xFFFFFFFFu;  // Philox ctr word 1 of synthetic-input draws
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11).  The key is kernel-uniform, so the key
+// schedule lives in SGPRs; each round is 2 x v_mad_u64_u32 + 2 x v_xor3_b32.
+// ---------------------------------------------------------------------------
+struct P4 {
+    uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ P4 philox10(P4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+        P4 n;
+        n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+        n.y = (uint32_t)p1;
+        n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+        n.w = (uint32_t)p0;
+        c = n;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+
+// Lie words of slots 2*pair and 2*pair+1 at level k for global trial word gw.
+__device__ __forceinline__ void lie_pair(uint64_t seed, uint32_t k, uint32_t pair, uint64_t gw,
+                                         uint64_t& lie0, uint64_t& lie1) {
+    P4 o = philox10(P4{pair, k, (uint32_t)gw, (uint32_t)(gw >> 32)}, (uint32_t)seed,
+                    (uint32_t)(seed >> 32));
+    lie0 = (uint64_t)o.y << 32 | o.x;
+    lie1 = (uint64_t)o.w << 32 | o.z;
+}
+
+__device__ __forceinline__ uint32_t mulhi_range(uint32_t u, uint32_t range) {
+    return (uint32_t)(((uint64_t)u * range) >> 32);
+}
+
+// ---------------------------------------------------------------------------
+// Fast unsigned division by a launch-uniform divisor (Granlund-Montgomery).
+// ---------------------------------------------------------------------------
+struct FastDiv {
+    uint32_t d, mul, shift;  // shift == 0xFFFFFFFF encodes d == 1
+};
+
+__host__ inline FastDiv make_fastdiv(uint32_t d) {
+    FastDiv f{d, 0, 0};
+    if (d <= 1) {  // d == 0 never divides: callers skip empty levels
+        f.shift = 0xFFFFFFFFu;
+        return f;
+    }
+    uint32_t l = 0;
+    while ((1ull << l) < d) ++l;
+    f.mul = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+    f.shift = l - 1;
+    return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+    if (f.shift == 0xFFFFFFFFu) return n;
+    const uint32_t t = __umulhi(n, f.mul);
+    return (t + ((n - t) >> 1)) >> f.shift;
+}
+
+// ---------------------------------------------------------------------------
+// Bit-sliced counters over 64-trial words.  P planes count up to 2^P - 1.
+// ---------------------------------------------------------------------------
+template <int P>
+struct Count {
+    uint64_t c[P];
+    __device__ __forceinline__ Count() {
+#pragma unroll
+        for (int i = 0; i < P; ++i) c[i] = 0;
+    }
+    __device__ __forceinline__ void add(uint64_t x) {
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+            const uint64_t t = c[i] & x;
+            c[i] ^= x;
+            x = t;
+        }
+    }
+    // lanes whose count >= T (T uniform)
+    __device__ __forceinline__ uint64_t ge(uint32_t T) const {
+        if (T == 0) return ~0ull;
+        if (T >= (1u << P)) return 0ull;
+        uint64_t gt = 0, eq = ~0ull;
+#pragma unroll
+        for (int i = P - 1; i >= 0; --i) {
+            if ((T >> i) & 1u) {
+                eq &= c[i];
+            } else {
+                gt |= eq & c[i];
+                eq &= ~c[i];
+            }
+        }
+        return gt | eq;
+    }
+};
+
+// planes needed to count s inputs
+__host__ __device__ inline int planes_for(uint32_t s) {
+    int p = 1;
+    while ((1u << p) <= s) ++p;
+    return p;
+}
+
+// ---------------------------------------------------------------------------
+// Per-trial epilogue: quorum (ba.py:197-253), IC1/IC2, bound, outputs.
+// A / U: lieutenant bitmasks (bit r, r = 1..n-1) of attack / undefined roots.
+// ---------------------------------------------------------------------------
+enum { C_TRIALS, C_AGREE, C_VAPPL, C_VALID, C_QR, C_QA, C_QU, C_UNDEF,
+       C_INB, C_VIOL, C_FTOT, C_ATT, C_NUM = 12 };
+
+__device__ __forceinline__ uint64_t part1by1(uint32_t v) {
+    uint64_t x = v;
+    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x << 2)) & 0x3333333333333333ull;
+    x = (x | (x << 1)) & 0x5555555555555555ull;
+    return x;
+}
+
+struct TrialCounts {
+    uint32_t v[C_NUM];
+    __device__ __forceinline__ TrialCounts() {
+#pragma unroll
+        for (int i = 0; i < C_NUM; ++i) v[i] = 0;
+    }
+};
+
+__device__ __forceinline__ void finish_trial(uint32_t n, uint32_t me, uint32_t fm, uint32_t oc,
+                                             uint32_t A, uint32_t U, uint64_t& dec,
+                                             uint32_t& out, TrialCounts& tc) {
+    const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
+    const uint32_t lts = all & ~1u;
+    fm &= all;
+    A &= lts;
+    U &= lts & ~A;
+    const uint32_t nA = __popc(A), nU = __popc(U), nR = (n - 1) - nA - nU;
+    const uint32_t na = nA + (oc == 1), nu = nU + (oc == 2), nr = nR + (oc == 0);
+    const uint32_t total = na + nr + nu;  // == n: every live general answers
+    uint32_t needed = 2 * ((total - 1) / 3) + 1;
+    if (total <= 3) needed = total - 1;
+    if (total == 1) needed = 1;
+    const uint32_t q = needed <= nr ? 0u : (needed <= na ? 1u : 2u);  // retreat first
+    const uint32_t loyal = lts & ~fm;
+    const uint32_t la = A & loyal, lu = U & loyal, lr = loyal & ~A & ~U;
+    const uint32_t agree = ((la != 0) + (lu != 0) + (lr != 0)) <= 1;
+    const uint32_t appl = (fm & 1u) == 0;
+    const uint32_t valid = appl && (oc == 1 ? la == loyal : lr == loyal);
+    const uint32_t nf = __popc(fm);
+    const uint32_t inb = nf <= me && n > 3 * me;
+    dec = part1by1(A >> 1) | (part1by1(U >> 1) << 1);
+    out = q | agree << 2 | appl << 3 | valid << 4 | inb << 5;
+    tc.v[C_TRIALS] += 1;
+    tc.v[C_AGREE] += agree;
+    tc.v[C_VAPPL] += appl;
+    tc.v[C_VALID] += valid;
+    tc.v[C_QR] += q == 0;
+    tc.v[C_QA] += q == 1;
+    tc.v[C_QU] += q == 2;
+    tc.v[C_UNDEF] += nU;
+    tc.v[C_INB] += inb;
+    tc.v[C_VIOL] += inb && (!agree || (appl && !valid));
+    tc.v[C_FTOT] += nf;
+    tc.v[C_ATT] += nA;
+}
+
+// Block-reduce per-thread counts into partial[blockIdx.x][0..15] (uint64).
+// Deterministic: integer sums, fixed reduction tree, no atomics.
+template <int BLOCK>
+__device__ __forceinline__ void block_counts_out(const TrialCounts& tc, uint64_t* partial) {
+    __shared__ uint64_t red[BLOCK / 64][C_NUM];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < C_NUM; ++i) {
+        uint64_t x = tc.v[i];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+        if (lane == 0) red[wv][i] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < 16) {
+        uint64_t s = 0;
+        if (threadIdx.x < C_NUM)
+            for (int w = 0; w < BLOCK / 64; ++w) s += red[w][threadIdx.x];
+        partial[(uint64_t)blockIdx.x * 16 + threadIdx.x] = s;
+    }
+}
+
+// Synthetic inputs (docs/SEMANTICS.md §4): u[i] = word i%4 of
+// Philox(ctr = (i/4, 0xFFFFFFFF, t_lo, t_hi)).  The partial Fisher-Yates
+// permutation lives in a per-thread LDS row (dynamic indices).
+struct GenSpec {
+    uint32_t faulty_mode, f, order_mode, order_value;
+};
+
+__device__ __forceinline__ uint32_t pick4(const P4& p, uint32_t i) {
+    return i == 0 ? p.x : (i == 1 ? p.y : (i == 2 ? p.z : p.w));
+}
+
+__device__ inline void gen_trial(uint32_t n, uint64_t seed, const GenSpec& g, uint64_t t,
+                                 uint8_t* perm_row, uint32_t* fmask, uint32_t* oc) {
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    P4 blk = philox10(P4{0u, kGenTag, (uint32_t)t, (uint32_t)(t >> 32)}, k0, k1);
+    if (oc) {
+        if (g.order_mode == 1) *oc = blk.x >> 31;
+        else if (g.order_mode == 2) *oc = g.order_value;
+    }
+    if (fmask && g.faulty_mode != 0) {
+        uint32_t nf;
+        if (g.faulty_mode == 1) {
+            const uint32_t fmax = g.f < n ? g.f : n;
+            nf = mulhi_range(blk.y, fmax + 1);
+        } else {
+            nf = g.f < n ? g.f : n;
+        }
+        for (uint32_t i = 0; i < n; ++i) perm_row[i] = (uint8_t)i;
+        uint32_t mask = 0, cur_call = 0;
+        for (uint32_t i = 0; i < nf; ++i) {
+            const uint32_t wi = 2 + i;
+            if ((wi >> 2) != cur_call) {
+                cur_call = wi >> 2;
+                blk = philox10(P4{cur_call, kGenTag, (uint32_t)t, (uint32_t)(t >> 32)}, k0, k1);
+            }
+            const uint32_t j = i + mulhi_range(pick4(blk, wi & 3), n - i);
+            const uint8_t tmp = perm_row[i];
+            perm_row[i] = perm_row[j];
+            perm_row[j] = tmp;
+            mask |= 1u << perm_row[i];
+        }
+        *fmask = mask;
+    }
+}
+
+}  // namespace ba

@@ -1,0 +1,355 @@
+// ba_levels.hip -- LEVELS engine: level-synchronous OM(m) over bit-packed HBM
+// arrays, plus the ba.py table-mode (OM(1) canonical draw order) kernel.
+//
+// Layout: level k is an array L_k[slot][word] of uint64, word-fastest, so the
+// 64 lanes of a wave touch 64 consecutive words of one slot (512 B, coalesced).
+//
+//   k_input     bit-slices per-trial inputs: F[g][w] = ballot(general g faulty)
+//   k_relay     L_k[x] = F[sender] ? lie(x) : L_{k-1}[parent(x)]   (ba.py:42-57, 263-277)
+//   k_majority  R_p[sigma.r] = [2a > s] over L_p[sigma.r] and R_{p+1}[sigma.j.r] (ba.py:159-195)
+//   k_epilogue  root majority (tie -> undefined), quorum, IC flags    (ba.py:188-255)
+#include "ba_engine.hpp"
+
+namespace ba {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ uint32_t grid_threads() { return gridDim.x * kBlock; }
+
+// ---------------------------------------------------------------------------
+// input bit-slicing: one wave per 64-trial word
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_input(uint32_t n, uint64_t seed, GenSpec gs,
+                                                  uint64_t t0, uint64_t ntrials,
+                                                  const uint32_t* __restrict__ faulty,
+                                                  const uint8_t* __restrict__ order,
+                                                  uint64_t* __restrict__ scratch, uint64_t W,
+                                                  uint64_t offF, uint64_t offOB, uint64_t offOO,
+                                                  uint64_t offVAL) {
+    __shared__ uint8_t perm[kBlock * kMaxN];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t words_per_grid = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t w = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); w < W;
+         w += words_per_grid) {
+        const uint64_t i = w * 64 + lane;  // trial index within the chunk
+        const bool valid = i < ntrials;
+        uint32_t fm = 0, oc = 0;
+        if (valid) {
+            if (gs.faulty_mode == 0) fm = faulty[i];
+            if (gs.order_mode == 0) oc = order[i];
+            gen_trial(n, seed, gs, t0 + i, perm + threadIdx.x * kMaxN,
+                      gs.faulty_mode == 0 ? nullptr : &fm, gs.order_mode == 0 ? nullptr : &oc);
+        }
+        uint64_t mine = 0;
+        for (uint32_t g = 0; g < n; ++g) {
+            const uint64_t b = __ballot(valid && ((fm >> g) & 1u));
+            if (lane == g) mine = b;
+        }
+        const uint64_t ob = __ballot(valid && oc == 1);
+        const uint64_t oo = __ballot(valid && oc == 2);
+        const uint64_t vv = __ballot(valid);
+        if (lane < n) scratch[offF + (uint64_t)lane * W + w] = mine;
+        if (lane == 0) {
+            scratch[offOB + w] = ob;
+            scratch[offOO + w] = oo;
+            scratch[offVAL + w] = vv;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// relay level k: one thread per (slot pair, word); one Philox call per thread
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_relay(uint32_t k, uint32_t S, uint32_t fanout,
+                                                  FastDiv divW, FastDiv divFan, uint32_t work,
+                                                  uint64_t seed, uint64_t gw0,
+                                                  const uint64_t* __restrict__ Lprev,
+                                                  uint64_t* __restrict__ Lk,
+                                                  const uint64_t* __restrict__ F,
+                                                  const uint8_t* __restrict__ sender) {
+    const uint32_t W = divW.d;
+    for (uint32_t idx = blockIdx.x * kBlock + threadIdx.x; idx < work; idx += grid_threads()) {
+        const uint32_t pair = fdiv(idx, divW);
+        const uint32_t w = idx - pair * W;
+        uint64_t lie[2];
+        lie_pair(seed, k, pair, gw0 + w, lie[0], lie[1]);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t x = 2 * pair + h;
+            if (x >= S) break;
+            uint64_t parent, fw;
+            if (k == 0) {  // commander -> lieutenant x (ba.py:263-277)
+                parent = Lprev[w];
+                fw = F[w];
+            } else {
+                const uint32_t y = fdiv(x, divFan);
+                parent = Lprev[(uint64_t)y * W + w];
+                fw = F[(uint64_t)sender[y] * W + w];
+            }
+            Lk[(uint64_t)x * W + w] = (fw & lie[h]) | (~fw & parent);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// inner majority level p (1 <= p < me): one thread per (slot, word)
+// ---------------------------------------------------------------------------
+template <int P>
+__global__ __launch_bounds__(kBlock) void k_majority(uint32_t s, FastDiv divW, FastDiv divS,
+                                                     uint32_t work,
+                                                     const uint64_t* __restrict__ Lp,
+                                                     const uint64_t* __restrict__ C,
+                                                     uint64_t* __restrict__ Rp) {
+    const uint32_t W = divW.d;
+    const uint32_t thr = s / 2 + 1;  // strict majority; inner tie -> non-attack
+    for (uint32_t idx = blockIdx.x * kBlock + threadIdx.x; idx < work; idx += grid_threads()) {
+        const uint32_t y = fdiv(idx, divW);
+        const uint32_t w = idx - y * W;
+        const uint32_t sr = fdiv(y, divS);
+        const uint32_t b = y - sr * s;
+        Count<P> cnt;
+        cnt.add(Lp[(uint64_t)y * W + w]);
+        const uint64_t base = (uint64_t)sr * s;
+        for (uint32_t a = 0; a < s; ++a) {
+            if (a == b) continue;
+            const uint64_t cs = (base + a) * (s - 1) + (b - (b > a));
+            cnt.add(C[cs * W + w]);
+        }
+        Rp[(uint64_t)y * W + w] = cnt.ge(thr);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// root majority + quorum epilogue: one wave per word
+// ---------------------------------------------------------------------------
+template <int P>
+__global__ __launch_bounds__(kBlock) void k_epilogue(uint32_t n, uint32_t me, uint64_t W,
+                                                     uint64_t ntrials,
+                                                     const uint64_t* __restrict__ scratch,
+                                                     uint64_t offF, uint64_t offOB, uint64_t offOO,
+                                                     uint64_t offVAL, uint64_t offL0,
+                                                     uint64_t offC1,
+                                                     uint64_t* __restrict__ decisions,
+                                                     uint8_t* __restrict__ outcome,
+                                                     uint64_t* __restrict__ partial) {
+    __shared__ uint64_t sA[kBlock / 64][kMaxN], sU[kBlock / 64][kMaxN], sF[kBlock / 64][kMaxN];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t L = n - 1;
+    TrialCounts tc;
+    const uint64_t words_per_grid = (uint64_t)gridDim.x * (kBlock / 64);
+    const uint64_t win = (W + (kBlock / 64) - 1) / (kBlock / 64) * (kBlock / 64);
+    for (uint64_t w0 = (uint64_t)blockIdx.x * (kBlock / 64); w0 < win; w0 += words_per_grid) {
+        const uint64_t w = w0 + wv;
+        const bool wok = w < W;
+        if (wok && lane < L) {  // root for lieutenant r = lane + 1 (bit-sliced)
+            const uint32_t b = lane;
+            Count<P> cnt;
+            cnt.add(scratch[offL0 + (uint64_t)b * W + w]);
+            if (me >= 1) {
+                for (uint32_t a = 0; a < L; ++a) {
+                    if (a == b) continue;
+                    const uint64_t cs = (uint64_t)a * (L - 1) + (b - (b > a));
+                    cnt.add(scratch[offC1 + cs * W + w]);
+                }
+            }
+            const uint64_t att = cnt.ge(L / 2 + 1);
+            const uint64_t tie = (L & 1u) ? 0ull : (cnt.ge(L / 2) & ~att);
+            sA[wv][lane] = att;
+            sU[wv][lane] = tie;
+        }
+        if (wok && lane < n) sF[wv][lane] = scratch[offF + (uint64_t)lane * W + w];
+        __syncthreads();
+        if (wok) {
+            const uint64_t i = w * 64 + lane;
+            const uint64_t vv = scratch[offVAL + w];
+            if ((vv >> lane) & 1ull) {
+                uint32_t A = 0, U = 0, fm = 0;
+                for (uint32_t b = 0; b < L; ++b) {
+                    A |= (uint32_t)((sA[wv][b] >> lane) & 1ull) << (b + 1);
+                    U |= (uint32_t)((sU[wv][b] >> lane) & 1ull) << (b + 1);
+                }
+                for (uint32_t g = 0; g < n; ++g) fm |= (uint32_t)((sF[wv][g] >> lane) & 1ull) << g;
+                const uint32_t ob = (uint32_t)(scratch[offOB + w] >> lane) & 1u;
+                const uint32_t oo = (uint32_t)(scratch[offOO + w] >> lane) & 1u;
+                const uint32_t oc = oo ? 2u : ob;
+                uint64_t dec;
+                uint32_t out;
+                finish_trial(n, me, fm, oc, A, U, dec, out, tc);
+                if (decisions) decisions[i] = dec;
+                if (outcome) outcome[i] = (uint8_t)out;
+            }
+        }
+        __syncthreads();
+    }
+    block_counts_out<kBlock>(tc, partial);
+}
+
+// ---------------------------------------------------------------------------
+// ba.py OM(1) in its canonical draw order (lie table), one thread per trial
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_table(uint32_t n, uint32_t relay, uint32_t me,
+                                                  uint64_t seed, GenSpec gs, uint64_t first_trial,
+                                                  uint64_t batch, const uint32_t* __restrict__ faulty,
+                                                  const uint8_t* __restrict__ order,
+                                                  const uint32_t* __restrict__ table,
+                                                  uint32_t stride, const uint32_t* __restrict__ poll,
+                                                  uint64_t* __restrict__ decisions,
+                                                  uint8_t* __restrict__ outcome,
+                                                  uint64_t* __restrict__ partial) {
+    __shared__ uint8_t perm[kBlock * kMaxN];
+    TrialCounts tc;
+    const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < batch;
+         i += (uint64_t)gridDim.x * kBlock) {
+        uint32_t fm = gs.faulty_mode == 0 ? faulty[i] : 0;
+        uint32_t oc = gs.order_mode == 0 ? order[i] : 0;
+        gen_trial(n, seed, gs, first_trial + i, perm + threadIdx.x * kMaxN,
+                  gs.faulty_mode == 0 ? nullptr : &fm, gs.order_mode == 0 ? nullptr : &oc);
+        fm &= all;
+        const uint32_t ob = oc == 1;
+        const uint32_t* row = table + i * stride;
+        uint32_t c = 0;
+        auto coin = [&]() -> uint32_t {
+            const uint32_t v = (row[c >> 5] >> (c & 31)) & 1u;
+            ++c;
+            return v;
+        };
+        uint32_t V = 0;
+        for (uint32_t r = 1; r < n; ++r) V |= ((fm & 1u) ? coin() : ob) << r;  // ba.py:263-277
+        const uint32_t pm = poll ? poll[i] & all & ~1u : 0u;
+        uint32_t A = 0, U = 0;
+        for (uint32_t r = 1; r < n; ++r) {  // ba.py:159-195, receiver-major
+            uint32_t a = (V >> r) & 1u, cnt = 1;
+            if (relay) {
+                if ((pm >> r) & 1u) {  // stale primary_port: the commander answers too
+                    a += (fm & 1u) ? coin() : ob;
+                    ++cnt;
+                }
+                for (uint32_t j = 1; j < n; ++j) {
+                    if (j == r) continue;
+                    a += ((fm >> j) & 1u) ? coin() : ((V >> j) & 1u);
+                    ++cnt;
+                }
+            }
+            if (2 * a > cnt) A |= 1u << r;
+            else if (2 * a == cnt) U |= 1u << r;
+        }
+        uint64_t dec;
+        uint32_t out;
+        finish_trial(n, me, fm, oc, A, U, dec, out, tc);
+        if (decisions) decisions[i] = dec;
+        if (outcome) outcome[i] = (uint8_t)out;
+    }
+    block_counts_out<kBlock>(tc, partial);
+}
+
+__global__ void k_reduce(const uint64_t* __restrict__ partial, int rows,
+                         uint64_t* __restrict__ counters) {
+    const int j = threadIdx.x;
+    if (j >= 16) return;
+    uint64_t s = 0;
+    for (int r = 0; r < rows; ++r) s += partial[(uint64_t)r * 16 + j];
+    counters[j] += s;
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+static uint32_t blocks_for(uint64_t work, uint32_t cap) {
+    uint64_t b = (work + kBlock - 1) / kBlock;
+    if (b < 1) b = 1;
+    return (uint32_t)(b < cap ? b : cap);
+}
+
+hipError_t launch_reduce(const uint64_t* partials, int rows, uint64_t* counters, hipStream_t s) {
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(64), 0, s, partials, rows, counters);
+    return hipGetLastError();
+}
+
+hipError_t launch_table(const RunArgs& a, uint64_t* partials) {
+    const uint32_t blocks = blocks_for(a.batch, kPartialRows);
+    ProfScope ps(a.prof, "k_table", a.stream);
+    hipLaunchKernelGGL(k_table, dim3(blocks), dim3(kBlock), 0, a.stream, a.n, (uint32_t)(a.m >= 1),
+                       a.me, a.seed, a.gen, a.first_trial, a.batch, a.faulty, a.order, a.table,
+                       a.table_stride, a.poll, a.decisions, a.outcome, partials);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_reduce(partials, (int)blocks, a.counters, a.stream);
+}
+
+template <int P>
+static void launch_majority_p(uint32_t s, uint32_t W, uint32_t work, const uint64_t* Lp,
+                              const uint64_t* C, uint64_t* Rp, hipStream_t st) {
+    hipLaunchKernelGGL(k_majority<P>, dim3(blocks_for(work, 16384)), dim3(kBlock), 0, st, s,
+                       make_fastdiv(W), make_fastdiv(s), work, Lp, C, Rp);
+}
+
+template <int P>
+static void launch_epilogue_p(uint32_t blocks, const RunArgs& a, uint64_t W, uint64_t nt,
+                              const uint64_t* scratch, const LevelsLayout& lay, uint64_t offC1,
+                              uint64_t* dec, uint8_t* out, uint64_t* partials) {
+    hipLaunchKernelGGL(k_epilogue<P>, dim3(blocks), dim3(kBlock), 0, a.stream, a.n, a.me, W, nt,
+                       scratch, lay.F, lay.OB, lay.OO, lay.VAL, lay.Lk[0], offC1, dec, out,
+                       partials);
+}
+
+hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_t* d_sender,
+                               uint64_t* scratch, const LevelsLayout& lay, uint64_t trial0,
+                               uint64_t ntrials, uint64_t* partials) {
+    const uint64_t W = (ntrials + 63) / 64;
+    const uint64_t gw0 = (a.first_trial + trial0) / 64;
+    hipStream_t st = a.stream;
+    { ProfScope ps(a.prof, "k_input", st);
+    hipLaunchKernelGGL(k_input, dim3(blocks_for(W * 64, 4096)), dim3(kBlock), 0, st, a.n, a.seed,
+                       a.gen, a.first_trial + trial0, ntrials,
+                       a.faulty ? a.faulty + trial0 : nullptr, a.order ? a.order + trial0 : nullptr,
+                       scratch, W, lay.F, lay.OB, lay.OO, lay.VAL); }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // relay, top-down (levels 0..me)
+    for (uint32_t k = 0; k <= g.me; ++k) {
+        const uint32_t S = (uint32_t)g.S[k];
+        const uint32_t work = (uint32_t)(((uint64_t)S + 1) / 2 * W);
+        const uint64_t* Lprev = k == 0 ? scratch + lay.OB : scratch + lay.Lk[k - 1];
+        const uint8_t* snd = k == 0 ? nullptr : d_sender + g.sender_off[k - 1];
+        ProfScope ps(a.prof, k == g.me ? "k_relay_leaf" : "k_relay_inner", st);
+        hipLaunchKernelGGL(k_relay, dim3(blocks_for(work, 16384)), dim3(kBlock), 0, st, k, S,
+                           g.L - k, make_fastdiv((uint32_t)W), make_fastdiv(g.L - k), work, a.seed,
+                           gw0, Lprev, scratch + lay.Lk[k], scratch + lay.F, snd);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    // inner majorities, bottom-up (levels me-1..1)
+    for (int p = (int)g.me - 1; p >= 1; --p) {
+        const uint32_t s = g.L - (uint32_t)p;
+        const uint32_t work = (uint32_t)(g.S[p] * W);
+        const uint64_t* C = (p + 1 == (int)g.me) ? scratch + lay.Lk[p + 1] : scratch + lay.Rp[p + 1];
+        const uint64_t* Lp = scratch + lay.Lk[p];
+        uint64_t* Rp = scratch + lay.Rp[p];
+        ProfScope ps(a.prof, p + 1 == (int)g.me ? "k_majority_leaf" : "k_majority_inner", st);
+        switch (planes_for(s)) {
+            case 1: launch_majority_p<1>(s, (uint32_t)W, work, Lp, C, Rp, st); break;
+            case 2: launch_majority_p<2>(s, (uint32_t)W, work, Lp, C, Rp, st); break;
+            case 3: launch_majority_p<3>(s, (uint32_t)W, work, Lp, C, Rp, st); break;
+            case 4: launch_majority_p<4>(s, (uint32_t)W, work, Lp, C, Rp, st); break;
+            default: launch_majority_p<5>(s, (uint32_t)W, work, Lp, C, Rp, st); break;
+        }
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    // root + quorum epilogue
+    const uint64_t offC1 = g.me >= 2 ? lay.Rp[1] : (g.me == 1 ? lay.Lk[1] : 0);
+    const uint32_t blocks = blocks_for(W * 64, kPartialRows);
+    uint64_t* dec = a.decisions ? a.decisions + trial0 : nullptr;
+    uint8_t* out = a.outcome ? a.outcome + trial0 : nullptr;
+    { ProfScope ps(a.prof, "k_epilogue", st);
+    switch (planes_for(g.L)) {
+        case 1: launch_epilogue_p<1>(blocks, a, W, ntrials, scratch, lay, offC1, dec, out, partials); break;
+        case 2: launch_epilogue_p<2>(blocks, a, W, ntrials, scratch, lay, offC1, dec, out, partials); break;
+        case 3: launch_epilogue_p<3>(blocks, a, W, ntrials, scratch, lay, offC1, dec, out, partials); break;
+        case 4: launch_epilogue_p<4>(blocks, a, W, ntrials, scratch, lay, offC1, dec, out, partials); break;
+        default: launch_epilogue_p<5>(blocks, a, W, ntrials, scratch, lay, offC1, dec, out, partials); break;
+    } }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return launch_reduce(partials, (int)blocks, a.counters, st);
+}
+
+}  // namespace ba

@@ -159,6 +159,15 @@ int ba_run_trials_device(struct ba_ctx* ctx, const ba_params* p, uint64_t batch,
                          uint64_t* d_decisions, uint8_t* d_outcome, uint64_t* d_counters,
                          void* stream);
 
+/* Per-kernel timing (tracing aux subsystem; replaces nothing in ba.py, which
+ * only prints).  When enabled, every kernel the ctx launches is bracketed by
+ * HIP events on its launch stream; ba_profile_read syncs those events and
+ * returns the index-th kernel's name, launch count and summed milliseconds
+ * (BA_EINVAL past the last kernel).  Enabling/disabling clears the totals. */
+int ba_profile_enable(struct ba_ctx* ctx, int on);
+int ba_profile_read(struct ba_ctx* ctx, int index, char* name, int name_len,
+                    uint64_t* launches, double* total_ms);
+
 /* Tree geometry helpers (host only, no device needed). */
 uint64_t ba_tree_slots(uint32_t n, uint32_t m);             /* sum_k |L_k|       */
 uint64_t ba_level_slots(uint32_t n, uint32_t m, uint32_t k); /* |L_k|=P(n-1,k+1) */

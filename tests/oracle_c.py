@@ -1,0 +1,59 @@
+"""ctypes wrapper of the C oracle (oracle/ba_oracle.c) for the tests and bench.py's
+cpu_baseline leg.  Test infrastructure only."""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SO = os.path.join(ROOT, "oracle", "_build", "libba_oracle.so")
+COUNTER_NAMES = ["trials", "agreement", "validity_applicable", "validity", "quorum_retreat",
+                 "quorum_attack", "quorum_undetermined", "undefined_decisions", "in_bound",
+                 "bound_violations", "faulty_total", "attack_decisions"]
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(SO):
+            subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+        lib = ctypes.CDLL(SO)
+        u32, u64, vp = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p
+        lib.ba_oracle_run.argtypes = [u32, u32, u64, u32, u32, u32, u32, u32, u64, u32, u64,
+                                      vp, vp, vp, vp, vp, vp, vp, ctypes.c_int]
+        lib.ba_oracle_lie.argtypes = [u64, u64, u32, u64]
+        lib.ba_oracle_lie.restype = u32
+        lib.ba_oracle_philox.argtypes = [vp, vp, vp]
+        lib.ba_oracle_gen.argtypes = [u32, u64, u32, u32, u32, u32, u64, vp, vp]
+        _lib = lib
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+def run(n, m, batch, seed=0, lie_mode=0, faulty_mode=0, f=0, order_mode=0, order_value=1,
+        first_trial=0, faulty=None, order=None, table=None, poll=None, threads=0):
+    """Returns (decisions uint64[batch], outcome uint8[batch], counters dict)."""
+    lib = load()
+    faulty = None if faulty is None else np.ascontiguousarray(faulty, np.uint32)
+    order = None if order is None else np.ascontiguousarray(order, np.uint8)
+    stride = 0
+    if table is not None:
+        table = np.ascontiguousarray(table, np.uint32)
+        stride = table.shape[1]
+    poll = None if poll is None else np.ascontiguousarray(poll, np.uint32)
+    dec = np.zeros(batch, np.uint64)
+    out = np.zeros(batch, np.uint8)
+    cnt = np.zeros(16, np.uint64)
+    rc = lib.ba_oracle_run(n, m, seed, lie_mode, faulty_mode, f, order_mode, order_value,
+                           first_trial, stride, batch, _p(faulty), _p(order), _p(table), _p(poll),
+                           _p(dec), _p(out), _p(cnt), threads)
+    if rc != 0:
+        raise RuntimeError(f"oracle rc={rc}")
+    return dec, out, dict(zip(COUNTER_NAMES, [int(x) for x in cnt[:12]]))

@@ -1,0 +1,209 @@
+"""GPU parity tests: libba_hip.so (through its C ABI) against the oracle.
+
+Bit-exact on decisions, per-trial outcome bytes and run counters.  The oracle
+runs on the same seeded inputs at sizes it finishes in seconds; at the bench's
+full size (n=10, m=3, 1M trials) the checks are size-independent properties
+plus oracle spot-checks of sampled trial words."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_c
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+CODE = {"attack": 1, "retreat": 0, "undefined": 2}
+ENGINES = [2]  # BA_ENGINE_LEVELS (FUSED joins when built)
+
+
+def _engines():
+    from ba_amd import lib as L
+    return [e for e in (L.ENGINE_FUSED, L.ENGINE_LEVELS) if e in ENGINES]
+
+
+def dec_codes(word, n):
+    return [(int(word) >> (2 * r)) & 3 for r in range(n - 1)]
+
+
+# --- bit-exact vs ba.py (canonical schedule, MT19937 coins in draw order) ----------
+def test_table_mode_matches_ba_py(engine):
+    from ba_amd import lib as L
+    cases = json.load(open(os.path.join(GOLD, "om1_cases.json")))["cases"]
+    by_n = {}
+    for c in cases:
+        by_n.setdefault(len(c["ids"]), []).append(c)
+    checked = 0
+    for n, cs in sorted(by_n.items()):
+        fm = [sum(1 << i for i, f in enumerate(c["faulty"]) if f) for c in cs]
+        pm = [sum(1 << i for i, f in enumerate(c["polls_commander"]) if f) for c in cs]
+        oc = [CODE.get(c["order"], 2) for c in cs]
+        tab = L.pack_coins([c["coins"] for c in cs], n)
+        res = engine.run(n, 1, len(cs), lie_mode=L.LIE_TABLE, faulty=fm, order=oc, table=tab,
+                         poll=pm)
+        od, oo, ocnt = oracle_c.run(n, 1, len(cs), lie_mode=1, faulty=fm, order=oc, table=tab,
+                                    poll=pm)
+        for j, c in enumerate(cs):
+            assert dec_codes(res.decisions[j], n) == [CODE[x] for x in c["majorities"][1:]], c["case"]
+            q = c["quorum_line"]
+            eq = 0 if "order: retreat!" in q else (1 if "order: attack!" in q else 2)
+            assert int(res.outcome[j]) & 3 == eq, c["case"]
+            checked += 1
+        assert np.array_equal(res.outcome, oo)
+        assert {k: res.counters[k] for k in ocnt} == ocnt
+    assert checked == len(cases)
+
+
+# --- Philox mode vs the C oracle ------------------------------------------------
+CONFIGS = [(1, 1), (2, 1), (3, 1), (4, 1), (4, 2), (5, 2), (6, 3), (7, 2), (7, 3), (8, 0),
+           (9, 3), (10, 1), (10, 2), (10, 3), (11, 2), (13, 2), (16, 1), (17, 1), (32, 1),
+           (20, 2), (12, 4)]
+
+
+@pytest.mark.parametrize("n,m", CONFIGS)
+def test_philox_random_sets_bit_exact(engine, n, m):
+    from ba_amd import lib as L
+    B = 777 if n <= 13 else 200
+    kw = dict(seed=0xBA5EED, faulty_mode=L.FAULTY_RANDOM, f=max(1, (n - 1) // 3 + 1),
+              order_mode=L.ORDER_RANDOM, first_trial=64 * 1000)
+    od, oo, ocnt = oracle_c.run(n, m, B, **kw)
+    for eng in _engines():
+        res = engine.run(n, m, B, engine=eng, **kw)
+        assert np.array_equal(res.decisions, od), (n, m, eng)
+        assert np.array_equal(res.outcome, oo), (n, m, eng)
+        assert {k: res.counters[k] for k in ocnt} == ocnt
+
+
+@pytest.mark.parametrize("n,m", [(4, 1), (10, 3), (16, 2), (32, 1), (5, 3)])
+def test_given_inputs_and_other_orders(engine, n, m):
+    rng = np.random.default_rng(n * 100 + m)
+    B = 333
+    fm = rng.integers(0, 1 << n, B, dtype=np.uint64).astype(np.uint32)
+    fm &= rng.integers(0, 1 << n, B, dtype=np.uint64).astype(np.uint32)  # sparser sets
+    oc = rng.choice([0, 1, 2], B).astype(np.uint8)
+    od, oo, ocnt = oracle_c.run(n, m, B, seed=42, faulty=fm, order=oc, first_trial=128)
+    for eng in _engines():
+        res = engine.run(n, m, B, seed=42, faulty=fm, order=oc, first_trial=128, engine=eng)
+        assert np.array_equal(res.decisions, od)
+        assert np.array_equal(res.outcome, oo)
+        assert {k: res.counters[k] for k in ocnt} == ocnt
+
+
+def test_faulty_fraction_sweep_counters(engine):
+    """Config 4 shape (n=10, m=3, exactly f faulty) at oracle-checkable size."""
+    from ba_amd import lib as L
+    for f in range(0, 5):
+        kw = dict(seed=0xBA5EED, faulty_mode=L.FAULTY_EXACT, f=f, order_mode=L.ORDER_RANDOM)
+        _, _, ocnt = oracle_c.run(10, 3, 1024, **kw)
+        res = engine.run(10, 3, 1024, want_decisions=False, want_outcome=False, **kw)
+        assert {k: res.counters[k] for k in ocnt} == ocnt
+        if f <= 3:
+            assert ocnt["bound_violations"] == 0
+
+
+def test_sharding_invariance(engine):
+    """Trials are keyed by global index: any split over calls/ranks gives the same bits."""
+    from ba_amd import lib as L
+    kw = dict(seed=7, faulty_mode=L.FAULTY_RANDOM, f=3, order_mode=L.ORDER_RANDOM)
+    full = engine.run(10, 3, 64 * 40, **kw)
+    parts = [engine.run(10, 3, 64 * 10, first_trial=64 * 10 * i, **kw) for i in range(4)]
+    assert np.array_equal(full.decisions, np.concatenate([p.decisions for p in parts]))
+    tot = {k: sum(p.counters[k] for p in parts) for k in full.counters}
+    assert tot == full.counters
+
+
+def test_levels_chunking(monkeypatch):
+    """A small scratch budget forces many chunks; results must not change."""
+    from ba_amd import lib as L
+    kw = dict(seed=3, faulty_mode=L.FAULTY_RANDOM, f=3, order_mode=L.ORDER_RANDOM,
+              engine=L.ENGINE_LEVELS)
+    e1 = L.Engine(0)
+    ref = e1.run(10, 3, 5000, **kw)
+    e1.close()
+    monkeypatch.setenv("BA_SCRATCH_BYTES", str(40 * 1024 * 8 * 5))  # ~5 words per chunk
+    e2 = L.Engine(0)
+    got = e2.run(10, 3, 5000, **kw)
+    e2.close()
+    assert np.array_equal(ref.decisions, got.decisions)
+    assert ref.counters == got.counters
+
+
+def test_single_huge_instance_n16_m5(engine):
+    """Config 5 shape: one OM(5) instance over 16 generals (4M tree slots)."""
+    from ba_amd import lib as L
+    fm = np.array([0b0000100000100110], np.uint32)  # generals 1, 2, 5, 11 faulty (f=4 <= 5)
+    od, oo, ocnt = oracle_c.run(16, 5, 1, seed=99, faulty=fm, order=[1], first_trial=0)
+    res = engine.run(16, 5, 1, seed=99, faulty=fm, order=[1], engine=L.ENGINE_LEVELS)
+    assert np.array_equal(res.decisions, od)
+    assert np.array_equal(res.outcome, oo)
+
+
+def test_n13_m4_batch(engine):
+    from ba_amd import lib as L
+    kw = dict(seed=0xBA5EED, faulty_mode=L.FAULTY_RANDOM, f=4, order_mode=L.ORDER_RANDOM,
+              first_trial=64 * 77)
+    od, oo, ocnt = oracle_c.run(13, 4, 130, **kw)
+    for eng in _engines():
+        res = engine.run(13, 4, 130, engine=eng, **kw)
+        assert np.array_equal(res.decisions, od)
+        assert {k: res.counters[k] for k in ocnt} == ocnt
+
+
+def test_bench_size_properties(engine):
+    """n=10, m=3, 1M trials (BASELINE config 2): size-independent invariants +
+    oracle spot-checks of three sampled 64-trial words."""
+    from ba_amd import lib as L
+    B = 1 << 20
+    kw = dict(seed=0xBA5EED, faulty_mode=L.FAULTY_RANDOM, f=3, order_mode=L.ORDER_RANDOM)
+    res = engine.run(10, 3, B, **kw)
+    c = res.counters
+    assert c["trials"] == B
+    assert c["quorum_retreat"] + c["quorum_attack"] + c["quorum_undetermined"] == B
+    assert c["in_bound"] == B and c["bound_violations"] == 0  # f <= 3 = m, n = 10 > 9
+    assert c["agreement"] == B
+    assert c["validity"] == c["validity_applicable"]
+    assert c["undefined_decisions"] == 0
+    # f ~ U{0..3}: mean 1.5 +- 5 sigma
+    assert abs(c["faulty_total"] / B - 1.5) < 5 * np.sqrt(1.25 / B)
+    for w in (0, 7777, B // 64 - 1):
+        od, oo, _ = oracle_c.run(10, 3, 64, first_trial=64 * w, **kw)
+        assert np.array_equal(res.decisions[64 * w:64 * w + 64], od), w
+        assert np.array_equal(res.outcome[64 * w:64 * w + 64], oo), w
+
+
+def test_device_api_accumulates(engine):
+    import torch
+    from ba_amd import lib as L
+    B = 4096
+    p = L.make_params(10, 3, seed=1, faulty_mode=L.FAULTY_RANDOM, f=3, order_mode=L.ORDER_RANDOM)
+    dec = torch.zeros(B, dtype=torch.int64, device="cuda")
+    cnt = torch.zeros(16, dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream()
+    engine.run_device(p, B, d_decisions=dec.data_ptr(), d_counters=cnt.data_ptr(), stream=s.cuda_stream)
+    engine.run_device(p, B, d_decisions=dec.data_ptr(), d_counters=cnt.data_ptr(), stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    ref = engine.run(10, 3, B, seed=1, faulty_mode=L.FAULTY_RANDOM, f=3, order_mode=L.ORDER_RANDOM)
+    assert np.array_equal(dec.cpu().numpy().view(np.uint64), ref.decisions)
+    got = cnt.cpu().numpy()
+    assert int(got[0]) == 2 * B and int(got[1]) == 2 * ref.counters["agreement"]
+
+
+def test_errors(engine):
+    from ba_amd import lib as L
+    with pytest.raises(L.BAError) as ei:
+        engine.run(5, 2, 4, lie_mode=L.LIE_TABLE, faulty=[0] * 4, order=[1] * 4,
+                   table=np.zeros((4, 1), np.uint32))
+    assert ei.value.code == L.ENOTSUP
+    with pytest.raises(L.BAError) as ei:
+        engine.run(5, 1, 4, first_trial=5, faulty=[0] * 4, order=[1] * 4)
+    assert ei.value.code == L.EINVAL
+    with pytest.raises(L.BAError) as ei:
+        engine.run(0, 1, 4, faulty=[0] * 4, order=[1] * 4)
+    assert ei.value.code == L.EINVAL
+    with pytest.raises(L.BAError) as ei:
+        engine.run(5, 1, 4, faulty_mode=L.FAULTY_GIVEN, order=[1] * 4)
+    assert ei.value.code == L.EINVAL
+    res = engine.run(5, 1, 0, faulty=[], order=[])
+    assert res.counters["trials"] == 0

@@ -1,0 +1,66 @@
+"""CPU tests of the C-ABI library: it loads, exports every symbol include/ba.h
+declares, and answers the device-free geometry queries.  No compute calls."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SO = os.path.join(ROOT, "byzantine-agreement_amd", "ba_amd", "libba_hip.so")
+
+
+def header_functions():
+    hdr = open(os.path.join(ROOT, "include", "ba.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    return sorted(set(re.findall(r"\b(ba_\w+)\s*\(", hdr)))
+
+
+def test_library_built():
+    assert os.path.exists(SO), "run __graft_entry__.build() / make -C byzantine-agreement_amd"
+
+
+def test_exports_every_header_symbol():
+    from ba_amd import lib as L
+    lib = L.load()
+    funcs = header_functions()
+    assert set(funcs) == set(L.EXPORTS)
+    for f in funcs:
+        assert hasattr(lib, f), f
+    syms = subprocess.run(["nm", "-D", "--defined-only", SO], capture_output=True, text=True,
+                          check=True).stdout
+    for f in funcs:
+        assert re.search(rf"\bT {f}$", syms, re.M), f
+
+
+def test_gfx950_code_object():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", SO],
+                         capture_output=True, text=True).stdout
+    r = subprocess.run(["strings", SO], capture_output=True, text=True).stdout
+    assert "gfx950" in out or "gfx950" in r
+
+
+def test_geometry_queries():
+    from ba_amd import lib as L
+    lib = L.load()
+    assert lib.ba_version() == L.ABI_VERSION
+    assert [lib.ba_level_slots(10, 3, k) for k in range(5)] == [9, 72, 504, 3024, 0]
+    assert lib.ba_tree_slots(10, 3) == 3609
+    assert lib.ba_tree_slots(13, 4) == 108384
+    assert lib.ba_tree_slots(16, 5) == 3999675
+    assert lib.ba_tree_slots(4, 1) == 9
+    assert lib.ba_tree_slots(2, 5) == 1  # effective depth min(m, n-2)
+
+
+def test_no_device_fails_loudly():
+    """Without a HIP device the library refuses to run: there is no CPU path."""
+    from ba_amd import lib as L
+    import ctypes
+    lib = L.load()
+    n = ctypes.c_int(-1)
+    rc = lib.ba_device_count(ctypes.byref(n))
+    if rc == 0 and n.value > 0:
+        pytest.skip("a HIP device is visible")
+    with pytest.raises(L.BAError) as ei:
+        L.Engine(0)
+    assert ei.value.code == L.EDEVICE
