@@ -122,7 +122,10 @@ def main():
     dec = torch.empty(B, dtype=torch.int64, device=dev)
     out = torch.empty(B, dtype=torch.uint8, device=dev)
     cnt = torch.zeros(16, dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated (non-null) stream: the library launches every kernel on it, so
+    # the HIP events below bracket exactly the hot-path kernels
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
 
     def step(i):
         first = (i * world + rank) * B  # global trial index: weak scaling, disjoint shards

@@ -67,6 +67,15 @@ def load(path: str | None = None):
     if not os.path.exists(p):
         raise FileNotFoundError(f"{p} not built: run `make -C byzantine-agreement_amd` "
                                 f"or __graft_entry__.build()")
+    # torch's wheel bundles its own libamdhip64.so.7 (same soname as /opt/rocm's).
+    # Whichever loads first serves the whole process, so let torch's load first
+    # when it is installed: then torch tensors/streams and our kernels share one
+    # HIP runtime (device pointers and hipStream_t handles are passed across).
+    if os.environ.get("BA_NO_TORCH", "0") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     lib = ctypes.CDLL(p)
     vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
     lib.ba_version.restype = i32

@@ -87,6 +87,7 @@ hipError_t launch_table(const RunArgs& a, uint64_t* partials);
 hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_t* d_sender,
                                uint64_t* scratch, const LevelsLayout& lay, uint64_t trial0,
                                uint64_t ntrials, uint64_t* partials);
-hipError_t launch_reduce(const uint64_t* partials, int rows, uint64_t* counters, hipStream_t s);
+hipError_t launch_reduce(const uint64_t* partials, int rows, uint64_t* counters, hipStream_t s,
+                         Prof* prof);
 
 }  // namespace ba

@@ -152,8 +152,9 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(uint32_t n, uint32_t me, ui
                     cnt.add(scratch[offC1 + cs * W + w]);
                 }
             }
-            const uint64_t att = cnt.ge(L / 2 + 1);
-            const uint64_t tie = (L & 1u) ? 0ull : (cnt.ge(L / 2) & ~att);
+            const uint32_t c = me >= 1 ? L : 1u;  // OM(0): the direct value alone
+            const uint64_t att = cnt.ge(c / 2 + 1);
+            const uint64_t tie = (c & 1u) ? 0ull : (cnt.ge(c / 2) & ~att);
             sA[wv][lane] = att;
             sU[wv][lane] = tie;
         }
@@ -243,13 +244,24 @@ __global__ __launch_bounds__(kBlock) void k_table(uint32_t n, uint32_t relay, ui
     block_counts_out<kBlock>(tc, partial);
 }
 
-__global__ void k_reduce(const uint64_t* __restrict__ partial, int rows,
-                         uint64_t* __restrict__ counters) {
-    const int j = threadIdx.x;
-    if (j >= 16) return;
+// Sum the per-block counter rows: 64 row groups x 16 columns, then a fixed
+// LDS tree over the groups (deterministic integer sums).
+constexpr int kReduceThreads = 1024;
+__global__ __launch_bounds__(kReduceThreads) void k_reduce(const uint64_t* __restrict__ partial,
+                                                           int rows,
+                                                           uint64_t* __restrict__ counters) {
+    __shared__ uint64_t red[kReduceThreads];
+    const int t = threadIdx.x, col = t & 15, grp = t >> 4;
     uint64_t s = 0;
-    for (int r = 0; r < rows; ++r) s += partial[(uint64_t)r * 16 + j];
-    counters[j] += s;
+#pragma unroll 8
+    for (int r = grp; r < rows; r += kReduceThreads / 16) s += partial[(uint64_t)r * 16 + col];
+    red[t] = s;
+    __syncthreads();
+    for (int stride = kReduceThreads / 2; stride >= 16; stride >>= 1) {
+        if (t < stride) red[t] += red[t + stride];
+        __syncthreads();
+    }
+    if (t < 16) counters[t] += red[t];
 }
 
 // ---------------------------------------------------------------------------
@@ -261,8 +273,10 @@ static uint32_t blocks_for(uint64_t work, uint32_t cap) {
     return (uint32_t)(b < cap ? b : cap);
 }
 
-hipError_t launch_reduce(const uint64_t* partials, int rows, uint64_t* counters, hipStream_t s) {
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(64), 0, s, partials, rows, counters);
+hipError_t launch_reduce(const uint64_t* partials, int rows, uint64_t* counters, hipStream_t s,
+                         Prof* prof) {
+    ProfScope ps(prof, "k_reduce", s);
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, s, partials, rows, counters);
     return hipGetLastError();
 }
 
@@ -274,7 +288,7 @@ hipError_t launch_table(const RunArgs& a, uint64_t* partials) {
                        a.table_stride, a.poll, a.decisions, a.outcome, partials);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return launch_reduce(partials, (int)blocks, a.counters, a.stream);
+    return launch_reduce(partials, (int)blocks, a.counters, a.stream, a.prof);
 }
 
 template <int P>
@@ -349,7 +363,7 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
         default: launch_epilogue_p<5>(blocks, a, W, ntrials, scratch, lay, offC1, dec, out, partials); break;
     } }
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    return launch_reduce(partials, (int)blocks, a.counters, st);
+    return launch_reduce(partials, (int)blocks, a.counters, st, a.prof);
 }
 
 }  // namespace ba

@@ -24,6 +24,18 @@ def _engines():
     return [e for e in (L.ENGINE_FUSED, L.ENGINE_LEVELS) if e in ENGINES]
 
 
+def same(a, b, what=""):
+    """Compact bit-exact comparison (first mismatches only, not whole arrays)."""
+    a, b = np.asarray(a), np.asarray(b)
+    if a.shape == b.shape and np.array_equal(a, b):
+        return
+    if a.shape != b.shape:
+        raise AssertionError(f"{what}: shape {a.shape} != {b.shape}")
+    idx = np.nonzero(a != b)[0]
+    raise AssertionError(f"{what}: {len(idx)} mismatches, first at {idx[:5].tolist()}: "
+                         f"got {a[idx[:5]].tolist()} want {b[idx[:5]].tolist()}")
+
+
 def dec_codes(word, n):
     return [(int(word) >> (2 * r)) & 3 for r in range(n - 1)]
 
@@ -51,7 +63,7 @@ def test_table_mode_matches_ba_py(engine):
             eq = 0 if "order: retreat!" in q else (1 if "order: attack!" in q else 2)
             assert int(res.outcome[j]) & 3 == eq, c["case"]
             checked += 1
-        assert np.array_equal(res.outcome, oo)
+        same(res.outcome, oo, '')
         assert {k: res.counters[k] for k in ocnt} == ocnt
     assert checked == len(cases)
 
@@ -71,8 +83,8 @@ def test_philox_random_sets_bit_exact(engine, n, m):
     od, oo, ocnt = oracle_c.run(n, m, B, **kw)
     for eng in _engines():
         res = engine.run(n, m, B, engine=eng, **kw)
-        assert np.array_equal(res.decisions, od), (n, m, eng)
-        assert np.array_equal(res.outcome, oo), (n, m, eng)
+        same(res.decisions, od, f"decisions n={n} m={m} engine={eng}")
+        same(res.outcome, oo, f"outcome n={n} m={m} engine={eng}")
         assert {k: res.counters[k] for k in ocnt} == ocnt
 
 
@@ -86,8 +98,8 @@ def test_given_inputs_and_other_orders(engine, n, m):
     od, oo, ocnt = oracle_c.run(n, m, B, seed=42, faulty=fm, order=oc, first_trial=128)
     for eng in _engines():
         res = engine.run(n, m, B, seed=42, faulty=fm, order=oc, first_trial=128, engine=eng)
-        assert np.array_equal(res.decisions, od)
-        assert np.array_equal(res.outcome, oo)
+        same(res.decisions, od, '')
+        same(res.outcome, oo, '')
         assert {k: res.counters[k] for k in ocnt} == ocnt
 
 
@@ -126,7 +138,7 @@ def test_levels_chunking(monkeypatch):
     e2 = L.Engine(0)
     got = e2.run(10, 3, 5000, **kw)
     e2.close()
-    assert np.array_equal(ref.decisions, got.decisions)
+    same(ref.decisions, got.decisions, '')
     assert ref.counters == got.counters
 
 
@@ -136,8 +148,8 @@ def test_single_huge_instance_n16_m5(engine):
     fm = np.array([0b0000100000100110], np.uint32)  # generals 1, 2, 5, 11 faulty (f=4 <= 5)
     od, oo, ocnt = oracle_c.run(16, 5, 1, seed=99, faulty=fm, order=[1], first_trial=0)
     res = engine.run(16, 5, 1, seed=99, faulty=fm, order=[1], engine=L.ENGINE_LEVELS)
-    assert np.array_equal(res.decisions, od)
-    assert np.array_equal(res.outcome, oo)
+    same(res.decisions, od, '')
+    same(res.outcome, oo, '')
 
 
 def test_n13_m4_batch(engine):
@@ -147,7 +159,7 @@ def test_n13_m4_batch(engine):
     od, oo, ocnt = oracle_c.run(13, 4, 130, **kw)
     for eng in _engines():
         res = engine.run(13, 4, 130, engine=eng, **kw)
-        assert np.array_equal(res.decisions, od)
+        same(res.decisions, od, '')
         assert {k: res.counters[k] for k in ocnt} == ocnt
 
 
@@ -169,8 +181,8 @@ def test_bench_size_properties(engine):
     assert abs(c["faulty_total"] / B - 1.5) < 5 * np.sqrt(1.25 / B)
     for w in (0, 7777, B // 64 - 1):
         od, oo, _ = oracle_c.run(10, 3, 64, first_trial=64 * w, **kw)
-        assert np.array_equal(res.decisions[64 * w:64 * w + 64], od), w
-        assert np.array_equal(res.outcome[64 * w:64 * w + 64], oo), w
+        same(res.decisions[64 * w:64 * w + 64], od, f"word {w}")
+        same(res.outcome[64 * w:64 * w + 64], oo, f"word {w}")
 
 
 def test_device_api_accumulates(engine):
@@ -185,7 +197,7 @@ def test_device_api_accumulates(engine):
     engine.run_device(p, B, d_decisions=dec.data_ptr(), d_counters=cnt.data_ptr(), stream=s.cuda_stream)
     torch.cuda.synchronize()
     ref = engine.run(10, 3, B, seed=1, faulty_mode=L.FAULTY_RANDOM, f=3, order_mode=L.ORDER_RANDOM)
-    assert np.array_equal(dec.cpu().numpy().view(np.uint64), ref.decisions)
+    same(dec.cpu().numpy().view(np.uint64), ref.decisions, '')
     got = cnt.cpu().numpy()
     assert int(got[0]) == 2 * B and int(got[1]) == 2 * ref.counters["agreement"]
 
