@@ -107,15 +107,20 @@ bool Geometry::build(uint32_t n_, uint32_t me_, uint64_t max_level_slots) {
     return true;
 }
 
-void LevelsLayout::plan(const Geometry& g, uint64_t W_) {
+void LevelsLayout::plan(const Geometry& g, uint64_t W_, bool leaf) {
     W = W_;
+    leaf_fused = leaf;
     uint64_t o = 0;
     F = o; o += (uint64_t)g.n * W;
     OB = o; o += W;
     OO = o; o += W;
     VAL = o; o += W;
     Lk.assign(g.me + 1, 0);
-    for (uint32_t k = 0; k <= g.me; ++k) { Lk[k] = o; o += g.S[k] * W; }
+    for (uint32_t k = 0; k <= g.me; ++k) {
+        if (leaf && k == g.me) break;  // generated on the fly by k_leaf
+        Lk[k] = o;
+        o += g.S[k] * W;
+    }
     Rp.assign(g.me + 1, 0);
     for (uint32_t p = 1; p < g.me; ++p) { Rp[p] = o; o += g.S[p] * W; }
     total = o;
@@ -150,6 +155,9 @@ struct DevBuf {
 struct GeoEntry {
     Geometry g;
     DevBuf sender;
+    bool fused_ok = false;
+    FusedPlan fp{};
+    DevBuf fplan;  // device copy of fp (k_fused reads it through a pointer)
 };
 
 struct ProfTotal {
@@ -161,6 +169,7 @@ struct ba_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     size_t scratch_budget = 8ull << 30;
+    bool leaf_fusion = true;  // LEVELS uses k_leaf when available (BA_NO_LEAF_FUSION=1: off)
     DevBuf scratch, partials, io_faulty, io_order, io_table, io_poll, io_dec, io_out, io_cnt;
     std::map<uint64_t, std::unique_ptr<GeoEntry>> geos;
     Prof prof;
@@ -252,6 +261,7 @@ extern "C" int ba_ctx_create(int device, ba_ctx** out) {
     auto* ctx = new ba_ctx();
     ctx->device = device;
     if (const char* s = getenv("BA_SCRATCH_BYTES")) ctx->scratch_budget = strtoull(s, nullptr, 0);
+    if (const char* s = getenv("BA_NO_LEAF_FUSION")) ctx->leaf_fusion = strcmp(s, "1") != 0;
     hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete ctx;
@@ -270,7 +280,10 @@ extern "C" void ba_ctx_destroy(ba_ctx* ctx) {
     for (DevBuf* b : {&ctx->scratch, &ctx->partials, &ctx->io_faulty, &ctx->io_order, &ctx->io_table,
                       &ctx->io_poll, &ctx->io_dec, &ctx->io_out, &ctx->io_cnt})
         b->release();
-    for (auto& kv : ctx->geos) kv.second->sender.release();
+    for (auto& kv : ctx->geos) {
+        kv.second->sender.release();
+        kv.second->fplan.release();
+    }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -290,9 +303,11 @@ extern "C" uint64_t ba_tree_slots(uint32_t n, uint32_t m) {
 }
 
 extern "C" int ba_engine_for(uint32_t n, uint32_t m) {
-    (void)n;
-    (void)m;
-    return BA_ENGINE_LEVELS;
+    if (n < 1 || n > BA_MAX_GENERALS || m > BA_MAX_DEPTH) return fail(BA_EINVAL, "n=%u m=%u", n, m);
+    Geometry g;
+    if (!g.build(n, effective_depth(n, m), 1ull << 31)) return BA_ENGINE_LEVELS;
+    FusedPlan fp;
+    return plan_fused(g, fp) ? BA_ENGINE_FUSED : BA_ENGINE_LEVELS;
 }
 
 // ---------------------------------------------------------------------------
@@ -343,6 +358,15 @@ static GeoEntry* geometry(ba_ctx* ctx, uint32_t n, uint32_t me, int* rc) {
                                  hipMemcpyHostToDevice);
         if (e != hipSuccess) {
             *rc = fail(BA_EDEVICE, "sender upload: %s", hipGetErrorString(e));
+            return nullptr;
+        }
+    }
+    ge->fused_ok = plan_fused(ge->g, ge->fp);
+    if (ge->fused_ok) {
+        if ((*rc = ge->fplan.grow(sizeof(FusedPlan))) != BA_OK) return nullptr;
+        hipError_t e = hipMemcpy(ge->fplan.p, &ge->fp, sizeof(FusedPlan), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            *rc = fail(BA_EDEVICE, "plan upload: %s", hipGetErrorString(e));
             return nullptr;
         }
     }
@@ -397,8 +421,19 @@ extern "C" int ba_run_trials_device(ba_ctx* ctx, const ba_params* p, uint64_t ba
     GeoEntry* ge = geometry(ctx, a.n, a.me, &rc);
     if (!ge) return rc;
     const Geometry& g = ge->g;
-    // chunk the batch so the scratch fits the budget and 32-bit indices hold
-    const uint64_t per_word = LevelsLayout::words_per_trial_word(g) * sizeof(uint64_t);
+    const bool fused_ok = ge->fused_ok;
+    if (p->engine == BA_ENGINE_FUSED && !fused_ok)
+        return fail(BA_ENOTSUP, "FUSED engine needs 2 <= m_eff <= %d and n - m_eff <= %d with the "
+                    "per-word tree within %llu B of LDS (n=%u, m_eff=%u)", kFusedMaxDepth,
+                    kMaxLeafS, (unsigned long long)kFusedLdsBudget, a.n, a.me);
+    if (fused_ok && p->engine != BA_ENGINE_LEVELS) {
+        HIP_TRY(launch_fused(a, g, ge->fp, (const FusedPlan*)ge->fplan.p,
+                             (const uint8_t*)ge->sender.p, partials));
+        return BA_OK;
+    }
+    // LEVELS: chunk the batch so the scratch fits the budget and 32-bit indices hold
+    const bool leaf = ctx->leaf_fusion && leaf_supported(g);
+    const uint64_t per_word = LevelsLayout::words_per_trial_word(g, leaf) * sizeof(uint64_t);
     uint64_t max_level = 0;
     for (uint64_t s : g.S) max_level = s > max_level ? s : max_level;
     uint64_t words = (batch + 63) / 64;
@@ -410,14 +445,14 @@ extern "C" int ba_run_trials_device(ba_ctx* ctx, const ba_params* p, uint64_t ba
         return fail(BA_ETOOBIG, "one 64-trial word needs %llu bytes of scratch (budget %zu)",
                     (unsigned long long)per_word, ctx->scratch_budget);
     LevelsLayout lay;
-    lay.plan(g, chunk);
+    lay.plan(g, chunk, leaf);
     if ((rc = ctx->scratch.grow(lay.total * sizeof(uint64_t))) != BA_OK) return rc;
     for (uint64_t w0 = 0; w0 < words; w0 += chunk) {
         const uint64_t wn = (words - w0) < chunk ? (words - w0) : chunk;
         const uint64_t trial0 = w0 * 64;
         const uint64_t nt = (batch - trial0) < wn * 64 ? (batch - trial0) : wn * 64;
         LevelsLayout cl;
-        cl.plan(g, wn);
+        cl.plan(g, wn, leaf);
         HIP_TRY(launch_levels_chunk(a, g, (const uint8_t*)ge->sender.p, (uint64_t*)ctx->scratch.p,
                                     cl, trial0, nt, partials));
     }

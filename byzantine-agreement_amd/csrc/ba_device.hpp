@@ -216,8 +216,26 @@ __device__ __forceinline__ uint32_t pick4(const P4& p, uint32_t i) {
     return i == 0 ? p.x : (i == 1 ? p.y : (i == 2 ? p.z : p.w));
 }
 
+// position of the j-th (0-based) set bit of v (j < popcount(v))
+__device__ __forceinline__ uint32_t select_bit(uint32_t v, uint32_t j) {
+    uint32_t base = 0;
+#pragma unroll
+    for (uint32_t s = 16; s >= 1; s >>= 1) {
+        const uint32_t lo = v & ((1u << s) - 1u);
+        const uint32_t c = __popc(lo);
+        if (j >= c) {
+            j -= c;
+            v >>= s;
+            base += s;
+        } else {
+            v = lo;
+        }
+    }
+    return base;
+}
+
 __device__ inline void gen_trial(uint32_t n, uint64_t seed, const GenSpec& g, uint64_t t,
-                                 uint8_t* perm_row, uint32_t* fmask, uint32_t* oc) {
+                                 uint32_t* fmask, uint32_t* oc) {
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     P4 blk = philox10(P4{0u, kGenTag, (uint32_t)t, (uint32_t)(t >> 32)}, k0, k1);
     if (oc) {
@@ -232,7 +250,8 @@ __device__ inline void gen_trial(uint32_t n, uint64_t seed, const GenSpec& g, ui
         } else {
             nf = g.f < n ? g.f : n;
         }
-        for (uint32_t i = 0; i < n; ++i) perm_row[i] = (uint8_t)i;
+        // sequential selection without replacement (docs/SEMANTICS.md §4)
+        const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
         uint32_t mask = 0, cur_call = 0;
         for (uint32_t i = 0; i < nf; ++i) {
             const uint32_t wi = 2 + i;
@@ -240,11 +259,8 @@ __device__ inline void gen_trial(uint32_t n, uint64_t seed, const GenSpec& g, ui
                 cur_call = wi >> 2;
                 blk = philox10(P4{cur_call, kGenTag, (uint32_t)t, (uint32_t)(t >> 32)}, k0, k1);
             }
-            const uint32_t j = i + mulhi_range(pick4(blk, wi & 3), n - i);
-            const uint8_t tmp = perm_row[i];
-            perm_row[i] = perm_row[j];
-            perm_row[j] = tmp;
-            mask |= 1u << perm_row[i];
+            const uint32_t j = mulhi_range(pick4(blk, wi & 3), n - i);
+            mask |= 1u << select_bit(all & ~mask, j);
         }
         *fmask = mask;
     }

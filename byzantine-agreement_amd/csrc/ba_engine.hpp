@@ -75,13 +75,35 @@ struct LevelsLayout {
     uint64_t F = 0, OB = 0, OO = 0, VAL = 0;
     std::vector<uint64_t> Lk, Rp;  // Rp[p] valid for 1 <= p < me
     uint64_t total = 0;
-    void plan(const Geometry& g, uint64_t W);
-    static uint64_t words_per_trial_word(const Geometry& g) {
-        return g.n + 3 + g.slots_total + g.inner_total;
+    bool leaf_fused = false;       // L_me not materialised (k_leaf)
+    void plan(const Geometry& g, uint64_t W, bool leaf);
+    static uint64_t words_per_trial_word(const Geometry& g, bool leaf) {
+        return g.n + 3 + g.slots_total + g.inner_total - (leaf ? g.S[g.me] : 0);
     }
 };
 
 constexpr int kPartialRows = 2048;  // max epilogue blocks per launch
+constexpr int kMaxLeafS = 12;       // leaf-fused kernels instantiated for S = n-me in 2..12
+constexpr int kFusedMaxDepth = 6;
+constexpr uint64_t kFusedLdsBudget = 48 * 1024;  // per block: three blocks per CU
+constexpr int kFusedMaxThreads = 576;            // 9 waves: <= 3 per SIMD, <= 168 VGPRs
+
+// LDS image of the FUSED engine (one per 64-trial word, WPB words per block).
+struct FusedPlan {
+    uint32_t n, me, wpb, threads, word_stride, lds_bytes, offRoot;
+    uint32_t S[kFusedMaxDepth + 1];        // level sizes
+    uint32_t offL[kFusedMaxDepth + 1];     // L_k, k = 0..me-2
+    uint32_t offR[kFusedMaxDepth + 1];     // R_p, p = 1..me-1
+    uint32_t snd_off[kFusedMaxDepth + 1];  // sender table offsets, levels 0..me-1
+};
+
+bool leaf_supported(const Geometry& g);
+bool plan_fused(const Geometry& g, FusedPlan& fp);
+hipError_t launch_leaf(const Geometry& g, uint64_t seed, uint64_t gw0, uint32_t W,
+                       const uint64_t* Lm1, const uint64_t* F, const uint8_t* d_sender,
+                       uint64_t* Rm1, hipStream_t st, Prof* prof);
+hipError_t launch_fused(const RunArgs& a, const Geometry& g, const FusedPlan& fp,
+                        const FusedPlan* d_fp, const uint8_t* d_sender, uint64_t* partials);
 
 hipError_t launch_table(const RunArgs& a, uint64_t* partials);
 hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_t* d_sender,

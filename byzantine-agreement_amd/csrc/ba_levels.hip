@@ -26,7 +26,6 @@ __global__ __launch_bounds__(kBlock) void k_input(uint32_t n, uint64_t seed, Gen
                                                   uint64_t* __restrict__ scratch, uint64_t W,
                                                   uint64_t offF, uint64_t offOB, uint64_t offOO,
                                                   uint64_t offVAL) {
-    __shared__ uint8_t perm[kBlock * kMaxN];
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t words_per_grid = (uint64_t)gridDim.x * (kBlock / 64);
     for (uint64_t w = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); w < W;
@@ -37,8 +36,8 @@ __global__ __launch_bounds__(kBlock) void k_input(uint32_t n, uint64_t seed, Gen
         if (valid) {
             if (gs.faulty_mode == 0) fm = faulty[i];
             if (gs.order_mode == 0) oc = order[i];
-            gen_trial(n, seed, gs, t0 + i, perm + threadIdx.x * kMaxN,
-                      gs.faulty_mode == 0 ? nullptr : &fm, gs.order_mode == 0 ? nullptr : &oc);
+            gen_trial(n, seed, gs, t0 + i, gs.faulty_mode == 0 ? nullptr : &fm,
+                      gs.order_mode == 0 ? nullptr : &oc);
         }
         uint64_t mine = 0;
         for (uint32_t g = 0; g < n; ++g) {
@@ -197,15 +196,14 @@ __global__ __launch_bounds__(kBlock) void k_table(uint32_t n, uint32_t relay, ui
                                                   uint64_t* __restrict__ decisions,
                                                   uint8_t* __restrict__ outcome,
                                                   uint64_t* __restrict__ partial) {
-    __shared__ uint8_t perm[kBlock * kMaxN];
     TrialCounts tc;
     const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < batch;
          i += (uint64_t)gridDim.x * kBlock) {
         uint32_t fm = gs.faulty_mode == 0 ? faulty[i] : 0;
         uint32_t oc = gs.order_mode == 0 ? order[i] : 0;
-        gen_trial(n, seed, gs, first_trial + i, perm + threadIdx.x * kMaxN,
-                  gs.faulty_mode == 0 ? nullptr : &fm, gs.order_mode == 0 ? nullptr : &oc);
+        gen_trial(n, seed, gs, first_trial + i, gs.faulty_mode == 0 ? nullptr : &fm,
+                  gs.order_mode == 0 ? nullptr : &oc);
         fm &= all;
         const uint32_t ob = oc == 1;
         const uint32_t* row = table + i * stride;
@@ -320,8 +318,10 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
                        scratch, W, lay.F, lay.OB, lay.OO, lay.VAL); }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    // relay, top-down (levels 0..me)
-    for (uint32_t k = 0; k <= g.me; ++k) {
+    // relay, top-down (levels 0..me, or 0..me-1 when the leaf level is fused
+    // into the leaf-parent majority and never materialised)
+    const uint32_t ktop = lay.leaf_fused ? g.me - 1 : g.me;
+    for (uint32_t k = 0; k <= ktop; ++k) {
         const uint32_t S = (uint32_t)g.S[k];
         const uint32_t work = (uint32_t)(((uint64_t)S + 1) / 2 * W);
         const uint64_t* Lprev = k == 0 ? scratch + lay.OB : scratch + lay.Lk[k - 1];
@@ -332,8 +332,13 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
                            gw0, Lprev, scratch + lay.Lk[k], scratch + lay.F, snd);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    // inner majorities, bottom-up (levels me-1..1)
-    for (int p = (int)g.me - 1; p >= 1; --p) {
+    if (lay.leaf_fused) {  // L_me generated on the fly: R_{me-1} straight from L_{me-1}
+        e = launch_leaf(g, a.seed, gw0, (uint32_t)W, scratch + lay.Lk[g.me - 1], scratch + lay.F,
+                        d_sender, scratch + lay.Rp[g.me - 1], st, a.prof);
+        if (e != hipSuccess) return e;
+    }
+    // inner majorities, bottom-up (levels me-1..1, or me-2..1 after k_leaf)
+    for (int p = (int)g.me - (lay.leaf_fused ? 2 : 1); p >= 1; --p) {
         const uint32_t s = g.L - (uint32_t)p;
         const uint32_t work = (uint32_t)(g.S[p] * W);
         const uint64_t* C = (p + 1 == (int)g.me) ? scratch + lay.Lk[p + 1] : scratch + lay.Rp[p + 1];

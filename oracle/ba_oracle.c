@@ -85,7 +85,8 @@ static uint32_t mulhi_range(uint32_t u, uint32_t range) {
 
 /* Synthetic inputs, SURVEY.md §8d: order ~ Bernoulli(1/2); f ~ U{0..fmax} (or
  * exactly f); faulty set = uniform f-subset of the n generals (the commander
- * may be faulty) by partial Fisher-Yates.  Random words u[i] are word i%4 of
+ * may be faulty) by sequential selection without replacement (the index form
+ * of a partial Fisher-Yates draw).  Random words u[i] are word i%4 of
  * Philox4x32-10(key = seed, ctr = (i/4, 0xFFFFFFFF, t_lo, t_hi)). */
 void ba_oracle_gen(uint32_t n, uint64_t seed, uint32_t faulty_mode, uint32_t f,
                    uint32_t order_mode, uint32_t order_value, uint64_t t,
@@ -109,13 +110,16 @@ void ba_oracle_gen(uint32_t n, uint64_t seed, uint32_t faulty_mode, uint32_t f,
         } else {
             nf = f < n ? f : n;
         }
-        int perm[MAXN];
-        for (uint32_t i = 0; i < n; ++i) perm[i] = (int)i;
+        /* sequential selection without replacement: step i takes the j-th
+         * (ascending) general not yet chosen, j = floor(u[2+i] * (n-i) / 2^32) */
         uint32_t mask = 0;
         for (uint32_t i = 0; i < nf; ++i) {
-            uint32_t j = i + mulhi_range(u[2 + i], n - i);
-            int tmp = perm[i]; perm[i] = perm[j]; perm[j] = tmp;
-            mask |= 1u << perm[i];
+            uint32_t j = mulhi_range(u[2 + i], n - i);
+            for (uint32_t g = 0; g < n; ++g) {
+                if ((mask >> g) & 1u) continue;
+                if (j == 0) { mask |= 1u << g; break; }
+                --j;
+            }
         }
         *faulty_mask = mask;
     }

@@ -65,12 +65,11 @@ def gen(n, seed, faulty_mode, f, order_mode, order_value, t):
             nf = (u[1] * (min(f, n) + 1)) >> 32
         else:
             nf = min(f, n)
-        perm = list(range(n))
         mask = 0
-        for i in range(nf):
-            j = i + ((u[2 + i] * (n - i)) >> 32)
-            perm[i], perm[j] = perm[j], perm[i]
-            mask |= 1 << perm[i]
+        for i in range(nf):  # j-th (ascending) general not chosen yet
+            j = (u[2 + i] * (n - i)) >> 32
+            free = [g for g in range(n) if not (mask >> g) & 1]
+            mask |= 1 << free[j]
     return mask, order
 
 

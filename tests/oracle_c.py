@@ -19,7 +19,8 @@ _lib = None
 def load():
     global _lib
     if _lib is None:
-        if not os.path.exists(SO):
+        src = os.path.join(ROOT, "oracle", "ba_oracle.c")
+        if not os.path.exists(SO) or os.path.getmtime(src) > os.path.getmtime(SO):
             subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
         lib = ctypes.CDLL(SO)
         u32, u64, vp = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p

@@ -16,12 +16,13 @@ pytestmark = pytest.mark.gpu
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 CODE = {"attack": 1, "retreat": 0, "undefined": 2}
-ENGINES = [2]  # BA_ENGINE_LEVELS (FUSED joins when built)
-
-
-def _engines():
+def _engines(n=None, m=None):
+    """Every engine that supports (n, m): LEVELS always, FUSED where it plans."""
     from ba_amd import lib as L
-    return [e for e in (L.ENGINE_FUSED, L.ENGINE_LEVELS) if e in ENGINES]
+    out = [L.ENGINE_LEVELS]
+    if n is not None and L.load().ba_engine_for(n, m) == L.ENGINE_FUSED:
+        out.insert(0, L.ENGINE_FUSED)
+    return out
 
 
 def same(a, b, what=""):
@@ -81,7 +82,7 @@ def test_philox_random_sets_bit_exact(engine, n, m):
     kw = dict(seed=0xBA5EED, faulty_mode=L.FAULTY_RANDOM, f=max(1, (n - 1) // 3 + 1),
               order_mode=L.ORDER_RANDOM, first_trial=64 * 1000)
     od, oo, ocnt = oracle_c.run(n, m, B, **kw)
-    for eng in _engines():
+    for eng in _engines(n, m):
         res = engine.run(n, m, B, engine=eng, **kw)
         same(res.decisions, od, f"decisions n={n} m={m} engine={eng}")
         same(res.outcome, oo, f"outcome n={n} m={m} engine={eng}")
@@ -96,7 +97,7 @@ def test_given_inputs_and_other_orders(engine, n, m):
     fm &= rng.integers(0, 1 << n, B, dtype=np.uint64).astype(np.uint32)  # sparser sets
     oc = rng.choice([0, 1, 2], B).astype(np.uint8)
     od, oo, ocnt = oracle_c.run(n, m, B, seed=42, faulty=fm, order=oc, first_trial=128)
-    for eng in _engines():
+    for eng in _engines(n, m):
         res = engine.run(n, m, B, seed=42, faulty=fm, order=oc, first_trial=128, engine=eng)
         same(res.decisions, od, '')
         same(res.outcome, oo, '')
@@ -157,7 +158,7 @@ def test_n13_m4_batch(engine):
     kw = dict(seed=0xBA5EED, faulty_mode=L.FAULTY_RANDOM, f=4, order_mode=L.ORDER_RANDOM,
               first_trial=64 * 77)
     od, oo, ocnt = oracle_c.run(13, 4, 130, **kw)
-    for eng in _engines():
+    for eng in _engines(13, 4):
         res = engine.run(13, 4, 130, engine=eng, **kw)
         same(res.decisions, od, '')
         assert {k: res.counters[k] for k in ocnt} == ocnt
@@ -219,3 +220,34 @@ def test_errors(engine):
     assert ei.value.code == L.EINVAL
     res = engine.run(5, 1, 0, faulty=[], order=[])
     assert res.counters["trials"] == 0
+
+
+@pytest.mark.parametrize("n,m", [(10, 3), (7, 2), (13, 4), (9, 4), (16, 3)])
+def test_engines_agree_with_and_without_leaf_fusion(monkeypatch, n, m):
+    """FUSED, LEVELS+k_leaf and LEVELS with the leaf level materialised
+    (BA_NO_LEAF_FUSION=1) are three code paths for one function."""
+    from ba_amd import lib as L
+    kw = dict(seed=0xC0FFEE, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1,
+              order_mode=L.ORDER_RANDOM, first_trial=64 * 5)
+    B = 64 * 37 + 5
+    outs = []
+    e1 = L.Engine(0)
+    for eng in _engines(n, m):
+        outs.append((f"engine {eng}", e1.run(n, m, B, engine=eng, **kw)))
+    e1.close()
+    monkeypatch.setenv("BA_NO_LEAF_FUSION", "1")
+    e2 = L.Engine(0)
+    outs.append(("levels, leaf materialised", e2.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)))
+    e2.close()
+    ref_name, ref = outs[-1]
+    for name, r in outs[:-1]:
+        same(r.decisions, ref.decisions, f"{name} vs {ref_name}")
+        same(r.outcome, ref.outcome, f"{name} vs {ref_name}")
+        assert r.counters == ref.counters, name
+    od, oo, _ = oracle_c.run(n, m, 128, **kw)
+    same(ref.decisions[:128], od, "vs oracle")
+
+
+def test_fused_engine_selected_for_bench_config():
+    from ba_amd import lib as L
+    assert L.load().ba_engine_for(10, 3) == L.ENGINE_FUSED
