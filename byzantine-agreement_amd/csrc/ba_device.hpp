@@ -234,15 +234,15 @@ __device__ __forceinline__ uint32_t select_bit(uint32_t v, uint32_t j) {
     return base;
 }
 
-__device__ inline void gen_trial(uint32_t n, uint64_t seed, const GenSpec& g, uint64_t t,
-                                 uint32_t* fmask, uint32_t* oc) {
+// Overwrites fmask unless faulty_mode is GIVEN and oc unless order_mode is GIVEN
+// (reference outputs: an address-taken local would live in scratch memory).
+__device__ __forceinline__ void gen_trial(uint32_t n, uint64_t seed, const GenSpec& g, uint64_t t,
+                                          uint32_t& fmask, uint32_t& oc) {
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     P4 blk = philox10(P4{0u, kGenTag, (uint32_t)t, (uint32_t)(t >> 32)}, k0, k1);
-    if (oc) {
-        if (g.order_mode == 1) *oc = blk.x >> 31;
-        else if (g.order_mode == 2) *oc = g.order_value;
-    }
-    if (fmask && g.faulty_mode != 0) {
+    if (g.order_mode == 1) oc = blk.x >> 31;
+    else if (g.order_mode == 2) oc = g.order_value;
+    if (g.faulty_mode != 0) {
         uint32_t nf;
         if (g.faulty_mode == 1) {
             const uint32_t fmax = g.f < n ? g.f : n;
@@ -262,7 +262,7 @@ __device__ inline void gen_trial(uint32_t n, uint64_t seed, const GenSpec& g, ui
             const uint32_t j = mulhi_range(pick4(blk, wi & 3), n - i);
             mask |= 1u << select_bit(all & ~mask, j);
         }
-        *fmask = mask;
+        fmask = mask;
     }
 }
 

@@ -85,8 +85,8 @@ struct LevelsLayout {
 constexpr int kPartialRows = 2048;  // max epilogue blocks per launch
 constexpr int kMaxLeafS = 12;       // leaf-fused kernels instantiated for S = n-me in 2..12
 constexpr int kFusedMaxDepth = 6;
-constexpr uint64_t kFusedLdsBudget = 48 * 1024;  // per block: three blocks per CU
-constexpr int kFusedMaxThreads = 576;            // 9 waves: <= 3 per SIMD, <= 168 VGPRs
+constexpr uint64_t kFusedLdsBudget = 39 * 1024;  // per block: four blocks per CU
+constexpr int kFusedThreads = 256;               // 4 waves: 4 blocks/CU at <= 128 VGPRs
 
 // LDS image of the FUSED engine (one per 64-trial word, WPB words per block).
 struct FusedPlan {

@@ -91,17 +91,19 @@ __global__ __launch_bounds__(256) void k_leaf(uint32_t me, uint64_t seed, uint64
 // arrays are indexed by runtime level numbers, which a by-value kernel
 // argument would turn into a private (scratch) copy.
 template <int S>
-__global__ __launch_bounds__(kFusedMaxThreads) void k_fused(
+__global__ __launch_bounds__(kFusedThreads, (S <= 7 ? 4 : 2)) void k_fused(
     const FusedPlan* __restrict__ fpp, uint64_t seed, GenSpec gs, uint64_t first_trial,
     uint64_t batch, const uint32_t* __restrict__ faulty, const uint8_t* __restrict__ order,
     const uint8_t* __restrict__ sender, uint64_t* __restrict__ decisions,
     uint8_t* __restrict__ outcome, uint64_t* __restrict__ partial) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    // run counters live in LDS (not in registers across the leaf stage)
+    __shared__ __attribute__((aligned(16))) unsigned long long blockcnt[16];
     const FusedPlan& fp = *fpp;
     const uint32_t n = fp.n, L = n - 1, me = fp.me, WPB = fp.wpb, T = blockDim.x;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t stride = fp.word_stride;  // uint64 words per trial word in LDS
-    TrialCounts tc;
+    if (tid < 16) blockcnt[tid] = 0;
     const uint64_t total_words = (batch + 63) / 64;
     const uint64_t groups = (total_words + WPB - 1) / WPB;
     for (uint64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
@@ -115,8 +117,7 @@ __global__ __launch_bounds__(kFusedMaxThreads) void k_fused(
             if (valid) {
                 if (gs.faulty_mode == 0) fm = faulty[i];
                 if (gs.order_mode == 0) oc = order[i];
-                gen_trial(n, seed, gs, first_trial + i, gs.faulty_mode == 0 ? nullptr : &fm,
-                          gs.order_mode == 0 ? nullptr : &oc);
+                gen_trial(n, seed, gs, first_trial + i, fm, oc);
             }
             uint64_t mine = 0;
             for (uint32_t g = 0; g < n; ++g) {
@@ -135,18 +136,21 @@ __global__ __launch_bounds__(kFusedMaxThreads) void k_fused(
         }
         __syncthreads();
         const uint64_t gwg = (first_trial >> 6) + w0;  // global word of lw = 0
-        // ---- B: top relay levels 0..me-2, one Philox per (slot pair, word) -------
-        for (uint32_t k = 0; k + 2 <= me; ++k) {
+        // ---- B: relay levels 0..me-1, one Philox per (slot pair, word) ----------
+        // level me-1 (the leaf blocks' diagonal) goes into the R_{me-1} area:
+        // each leaf block later reads its S words there before overwriting
+        // exactly those S words with its S majorities.
+        for (uint32_t k = 0; k + 1 <= me; ++k) {
+            const uint32_t outk = (k + 1 == me) ? fp.offR[me - 1] : fp.offL[k];
             const uint32_t Sk = fp.S[k], npair = (Sk + 1) / 2;
             for (uint32_t it = tid; it < npair * WPB; it += T) {
                 const uint32_t lw = it / npair, pair = it - lw * npair;
                 uint64_t* img = lds + (uint64_t)lw * stride;
-                uint64_t lie[2];
-                lie_pair(seed, k, pair, gwg + lw, lie[0], lie[1]);
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const uint32_t x = 2 * pair + h;
-                    if (x >= Sk) break;
+                uint64_t lie0, lie1;
+                lie_pair(seed, k, pair, gwg + lw, lie0, lie1);
+                static_for<0, 2>([&](auto h) {
+                    const uint32_t x = 2 * pair + h();
+                    if (x >= Sk) return;
                     uint64_t parent, fw;
                     if (k == 0) {
                         parent = img[n];
@@ -156,8 +160,9 @@ __global__ __launch_bounds__(kFusedMaxThreads) void k_fused(
                         parent = img[fp.offL[k - 1] + y];
                         fw = img[sender[fp.snd_off[k - 1] + y]];
                     }
-                    img[fp.offL[k] + x] = (fw & lie[h]) | (~fw & parent);
-                }
+                    const uint64_t lie = h() ? lie1 : lie0;
+                    img[outk + x] = (fw & lie) | (~fw & parent);
+                });
             }
             __syncthreads();
         }
@@ -168,29 +173,15 @@ __global__ __launch_bounds__(kFusedMaxThreads) void k_fused(
                 const uint32_t lw = it / Q, sr = it - lw * Q;
                 uint64_t* img = lds + (uint64_t)lw * stride;
                 const uint64_t gw = gwg + lw;
-                // level me-1: diag[a] = F[last(sigma)] ? lie : L_{me-2}[sigma]
-                const uint64_t par = img[fp.offL[me - 2] + sr];
-                const uint64_t fs = img[sender[fp.snd_off[me - 2] + sr]];
                 const uint32_t x0 = sr * S;
-                // S odd: x0 = sr*S has either parity, (S+1)/2 pairs cover the S
-                // slots from x0; S even: x0 is even and S/2 pairs suffice
-                constexpr int NPD = (S + 1) / 2;
-                uint64_t lw2[2 * NPD];
-                static_for<0, NPD>([&](auto q) {
-                    lie_pair(seed, me - 1, (x0 >> 1) + q(), gw, lw2[2 * q()], lw2[2 * q() + 1]);
-                });
-                const bool odd = x0 & 1u;
                 const uint32_t snd1 = fp.snd_off[me - 1] + x0;
+                const uint32_t offR = fp.offR[me - 1] + x0;  // L_{me-1}[sigma.*], then R_{me-1}
                 uint64_t diag[S], Fm[S], R[S];
                 static_for<0, S>([&](auto a) {
-                    uint64_t lie;
-                    if constexpr (S % 2 == 1) lie = odd ? lw2[a() + 1] : lw2[a()];
-                    else lie = lw2[a()];
-                    diag[a()] = (fs & lie) | (~fs & par);
+                    diag[a()] = img[offR + a()];
                     Fm[a()] = img[sender[snd1 + a()]];
                 });
                 leaf_block<S>(me, seed, gw, sr, diag, Fm, R);
-                const uint32_t offR = fp.offR[me - 1] + x0;
                 static_for<0, S>([&](auto b) { img[offR + b()] = R[b()]; });
             }
             __syncthreads();
@@ -234,6 +225,7 @@ __global__ __launch_bounds__(kFusedMaxThreads) void k_fused(
             const uint64_t* img = lds + (uint64_t)lw * stride;
             const uint64_t w = w0 + lw;
             const uint64_t i = w * 64 + lane;
+            TrialCounts tc;
             if (w < total_words && ((img[n + 2] >> lane) & 1ull)) {
                 uint32_t A = 0, U = 0, fm = 0;
                 for (uint32_t b = 0; b < L; ++b) {
@@ -249,25 +241,18 @@ __global__ __launch_bounds__(kFusedMaxThreads) void k_fused(
                 if (decisions) decisions[i] = dec;
                 if (outcome) outcome[i] = (uint8_t)out;
             }
+            // wave sum, then one LDS atomic per counter (integer: order-free)
+#pragma unroll
+            for (int c = 0; c < C_NUM; ++c) {
+                uint32_t x = tc.v[c];
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+                if (lane == 0 && x) atomicAdd(&blockcnt[c], (unsigned long long)x);
+            }
         }
         __syncthreads();
     }
-    // block counter row (fixed tree, deterministic)
-    __shared__ uint64_t red[16][C_NUM];
-#pragma unroll
-    for (int i = 0; i < C_NUM; ++i) {
-        uint64_t x = tc.v[i];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-        if (lane == 0) red[wv][i] = x;
-    }
-    __syncthreads();
-    if (tid < 16) {
-        uint64_t s = 0;
-        if (tid < C_NUM)
-            for (uint32_t w = 0; w < T / 64; ++w) s += red[w][tid];
-        partial[(uint64_t)blockIdx.x * 16 + tid] = s;
-    }
+    if (tid < 16) partial[(uint64_t)blockIdx.x * 16 + tid] = blockcnt[tid];
 }
 
 // ---------------------------------------------------------------------------
@@ -332,19 +317,22 @@ bool plan_fused(const Geometry& g, FusedPlan& fp) {
     const uint64_t bytes_per_word = (uint64_t)o * 8;
     const uint32_t Q = fp.S[g.me - 2];
     if (bytes_per_word > kFusedLdsBudget) return false;
-    // words per block: LDS image within budget, at most 16 words, and at most
-    // kFusedMaxThreads threads when every leaf block of every word gets its own
-    // thread (n=10, m=3: 72 leaf blocks x 8 words = 576 threads, 42 KiB)
-    uint32_t wpb = 16;
-    auto threads_for = [&](uint32_t w) {
-        uint32_t t = (Q * w + 63) / 64 * 64;
-        return t < 64 * w ? 64 * w : t;
-    };
-    while (wpb > 1 &&
-           (bytes_per_word * wpb > kFusedLdsBudget || threads_for(wpb) > (uint32_t)kFusedMaxThreads))
-        wpb >>= 1;
-    uint32_t T = threads_for(wpb);
-    if (T > (uint32_t)kFusedMaxThreads) T = kFusedMaxThreads / 64 * 64;  // leaf blocks take several passes
+    // words per block: the LDS image fits the budget, and the leaf stage (Q
+    // blocks per word over 256 threads) wastes the fewest thread-passes
+    // (n=10, m=3: 7 words -> 504 leaf blocks in two passes of 256, 98% busy)
+    const uint32_t T = kFusedThreads;
+    uint32_t wpb = 0;
+    double best = -1.0;
+    for (uint32_t w = 1; w <= 16; ++w) {
+        if (bytes_per_word * w > kFusedLdsBudget) break;
+        const uint32_t passes = (Q * w + T - 1) / T;
+        const double eff = (double)(Q * w) / (double)(passes * T) + 1e-3 * w;  // tie -> more words
+        if (eff > best) {
+            best = eff;
+            wpb = w;
+        }
+    }
+    if (wpb == 0) return false;
     fp.wpb = wpb;
     fp.threads = T;
     fp.lds_bytes = (uint32_t)(bytes_per_word * wpb);

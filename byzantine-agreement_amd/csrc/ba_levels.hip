@@ -36,8 +36,7 @@ __global__ __launch_bounds__(kBlock) void k_input(uint32_t n, uint64_t seed, Gen
         if (valid) {
             if (gs.faulty_mode == 0) fm = faulty[i];
             if (gs.order_mode == 0) oc = order[i];
-            gen_trial(n, seed, gs, t0 + i, gs.faulty_mode == 0 ? nullptr : &fm,
-                      gs.order_mode == 0 ? nullptr : &oc);
+            gen_trial(n, seed, gs, t0 + i, fm, oc);
         }
         uint64_t mine = 0;
         for (uint32_t g = 0; g < n; ++g) {
@@ -202,8 +201,7 @@ __global__ __launch_bounds__(kBlock) void k_table(uint32_t n, uint32_t relay, ui
          i += (uint64_t)gridDim.x * kBlock) {
         uint32_t fm = gs.faulty_mode == 0 ? faulty[i] : 0;
         uint32_t oc = gs.order_mode == 0 ? order[i] : 0;
-        gen_trial(n, seed, gs, first_trial + i, gs.faulty_mode == 0 ? nullptr : &fm,
-                  gs.order_mode == 0 ? nullptr : &oc);
+        gen_trial(n, seed, gs, first_trial + i, fm, oc);
         fm &= all;
         const uint32_t ob = oc == 1;
         const uint32_t* row = table + i * stride;
