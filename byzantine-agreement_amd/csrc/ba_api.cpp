@@ -104,6 +104,17 @@ bool Geometry::build(uint32_t n_, uint32_t me_, uint64_t max_level_slots) {
             }
         }
     }
+    members.clear();
+    const uint32_t S_leaf = n - me;
+    if (me >= 2 && S_leaf <= 12) {
+        members.assign(S[me - 2], 0);
+        for (uint64_t sr = 0; sr < S[me - 2]; ++sr) {
+            uint64_t packed = 0;
+            for (uint32_t a = 0; a < S_leaf; ++a)
+                packed |= (uint64_t)sender[sender_off[me - 1] + sr * S_leaf + a] << (5 * a);
+            members[sr] = packed;
+        }
+    }
     return true;
 }
 
@@ -157,7 +168,8 @@ struct GeoEntry {
     DevBuf sender;
     bool fused_ok = false;
     FusedPlan fp{};
-    DevBuf fplan;  // device copy of fp (k_fused reads it through a pointer)
+    DevBuf fplan;    // device copy of fp (k_fused reads it through a pointer)
+    DevBuf members;  // device copy of g.members
 };
 
 struct ProfTotal {
@@ -283,6 +295,7 @@ extern "C" void ba_ctx_destroy(ba_ctx* ctx) {
     for (auto& kv : ctx->geos) {
         kv.second->sender.release();
         kv.second->fplan.release();
+        kv.second->members.release();
     }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -361,6 +374,15 @@ static GeoEntry* geometry(ba_ctx* ctx, uint32_t n, uint32_t me, int* rc) {
             return nullptr;
         }
     }
+    if (!ge->g.members.empty()) {
+        const size_t mb = ge->g.members.size() * sizeof(uint64_t);
+        if ((*rc = ge->members.grow(mb)) != BA_OK) return nullptr;
+        hipError_t e = hipMemcpy(ge->members.p, ge->g.members.data(), mb, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            *rc = fail(BA_EDEVICE, "members upload: %s", hipGetErrorString(e));
+            return nullptr;
+        }
+    }
     ge->fused_ok = plan_fused(ge->g, ge->fp);
     if (ge->fused_ok) {
         if ((*rc = ge->fplan.grow(sizeof(FusedPlan))) != BA_OK) return nullptr;
@@ -421,6 +443,7 @@ extern "C" int ba_run_trials_device(ba_ctx* ctx, const ba_params* p, uint64_t ba
     GeoEntry* ge = geometry(ctx, a.n, a.me, &rc);
     if (!ge) return rc;
     const Geometry& g = ge->g;
+    a.members = (const uint64_t*)ge->members.p;
     const bool fused_ok = ge->fused_ok;
     if (p->engine == BA_ENGINE_FUSED && !fused_ok)
         return fail(BA_ENOTSUP, "FUSED engine needs 2 <= m_eff <= %d and n - m_eff <= %d with the "

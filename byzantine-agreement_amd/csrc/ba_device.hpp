@@ -145,9 +145,13 @@ struct TrialCounts {
     }
 };
 
-__device__ __forceinline__ void finish_trial(uint32_t n, uint32_t me, uint32_t fm, uint32_t oc,
-                                             uint32_t A, uint32_t U, uint64_t& dec,
-                                             uint32_t& out, TrialCounts& tc) {
+struct TrialResult {
+    uint64_t dec;
+    uint32_t out, nU, nf, nA;
+};
+
+__device__ __forceinline__ TrialResult trial_result(uint32_t n, uint32_t me, uint32_t fm,
+                                                    uint32_t oc, uint32_t A, uint32_t U) {
     const uint32_t all = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
     const uint32_t lts = all & ~1u;
     fm &= all;
@@ -167,8 +171,55 @@ __device__ __forceinline__ void finish_trial(uint32_t n, uint32_t me, uint32_t f
     const uint32_t valid = appl && (oc == 1 ? la == loyal : lr == loyal);
     const uint32_t nf = __popc(fm);
     const uint32_t inb = nf <= me && n > 3 * me;
-    dec = part1by1(A >> 1) | (part1by1(U >> 1) << 1);
-    out = q | agree << 2 | appl << 3 | valid << 4 | inb << 5;
+    TrialResult r;
+    r.dec = part1by1(A >> 1) | (part1by1(U >> 1) << 1);
+    r.out = q | agree << 2 | appl << 3 | valid << 4 | inb << 5;
+    r.nU = nU;
+    r.nf = nf;
+    r.nA = nA;
+    return r;
+}
+
+// Wave-level run counters from per-lane trial results: 0/1 flags by
+// ballot+popcount, small integers bit-sliced (5 ballots each); lane 0 adds
+// the wave's totals into a block counter array in LDS.
+__device__ __forceinline__ void wave_counts_add(bool live, const TrialResult& r,
+                                                unsigned long long* blockcnt) {
+    const uint32_t o = r.out;
+    const bool agree = (o >> 2) & 1, appl = (o >> 3) & 1, valid = (o >> 4) & 1, inb = (o >> 5) & 1;
+    const uint32_t q = o & 3;
+    uint64_t c[C_NUM];
+    c[C_TRIALS] = __popcll(__ballot(live));
+    c[C_AGREE] = __popcll(__ballot(live && agree));
+    c[C_VAPPL] = __popcll(__ballot(live && appl));
+    c[C_VALID] = __popcll(__ballot(live && valid));
+    c[C_QR] = __popcll(__ballot(live && q == 0));
+    c[C_QA] = __popcll(__ballot(live && q == 1));
+    c[C_QU] = __popcll(__ballot(live && q == 2));
+    c[C_INB] = __popcll(__ballot(live && inb));
+    c[C_VIOL] = __popcll(__ballot(live && inb && (!agree || (appl && !valid))));
+    c[C_UNDEF] = c[C_FTOT] = c[C_ATT] = 0;
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+        c[C_UNDEF] += (uint64_t)__popcll(__ballot(live && ((r.nU >> b) & 1u))) << b;
+        c[C_FTOT] += (uint64_t)__popcll(__ballot(live && ((r.nf >> b) & 1u))) << b;
+        c[C_ATT] += (uint64_t)__popcll(__ballot(live && ((r.nA >> b) & 1u))) << b;
+    }
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int i = 0; i < C_NUM; ++i)
+            if (c[i]) atomicAdd(&blockcnt[i], (unsigned long long)c[i]);
+    }
+}
+
+__device__ __forceinline__ void finish_trial(uint32_t n, uint32_t me, uint32_t fm, uint32_t oc,
+                                             uint32_t A, uint32_t U, uint64_t& dec,
+                                             uint32_t& out, TrialCounts& tc) {
+    const TrialResult r = trial_result(n, me, fm, oc, A, U);
+    dec = r.dec;
+    out = r.out;
+    const uint32_t q = r.out & 3, agree = (r.out >> 2) & 1, appl = (r.out >> 3) & 1;
+    const uint32_t valid = (r.out >> 4) & 1, inb = (r.out >> 5) & 1;
     tc.v[C_TRIALS] += 1;
     tc.v[C_AGREE] += agree;
     tc.v[C_VAPPL] += appl;
@@ -176,11 +227,11 @@ __device__ __forceinline__ void finish_trial(uint32_t n, uint32_t me, uint32_t f
     tc.v[C_QR] += q == 0;
     tc.v[C_QA] += q == 1;
     tc.v[C_QU] += q == 2;
-    tc.v[C_UNDEF] += nU;
+    tc.v[C_UNDEF] += r.nU;
     tc.v[C_INB] += inb;
     tc.v[C_VIOL] += inb && (!agree || (appl && !valid));
-    tc.v[C_FTOT] += nf;
-    tc.v[C_ATT] += nA;
+    tc.v[C_FTOT] += r.nf;
+    tc.v[C_ATT] += r.nA;
 }
 
 // Block-reduce per-thread counts into partial[blockIdx.x][0..15] (uint64).

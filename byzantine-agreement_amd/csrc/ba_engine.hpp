@@ -44,6 +44,7 @@ struct RunArgs {
     uint64_t* counters = nullptr;  // BA_NCOUNTERS, accumulated into
     hipStream_t stream = nullptr;
     Prof* prof = nullptr;
+    const uint64_t* members = nullptr;  // device copy of Geometry::members
 };
 
 struct ProfScope {  // RAII: times one launch when profiling is on
@@ -66,6 +67,9 @@ struct Geometry {
     std::vector<uint8_t> sender;       // general index of the last relayer of a slot
     uint64_t slots_total = 0;          // sum_k S[k]
     uint64_t inner_total = 0;          // sum_{1<=p<me} S[p] (inner majority levels)
+    // leaf blocks (me >= 2, S = n-me <= 12): for every prefix sigma at level
+    // me-2, the general ids of its S members packed 5 bits each, rank order
+    std::vector<uint64_t> members;
     bool build(uint32_t n, uint32_t me, uint64_t max_level_slots);
 };
 
@@ -100,7 +104,7 @@ struct FusedPlan {
 bool leaf_supported(const Geometry& g);
 bool plan_fused(const Geometry& g, FusedPlan& fp);
 hipError_t launch_leaf(const Geometry& g, uint64_t seed, uint64_t gw0, uint32_t W,
-                       const uint64_t* Lm1, const uint64_t* F, const uint8_t* d_sender,
+                       const uint64_t* Lm1, const uint64_t* F, const uint64_t* d_members,
                        uint64_t* Rm1, hipStream_t st, Prof* prof);
 hipError_t launch_fused(const RunArgs& a, const Geometry& g, const FusedPlan& fp,
                         const FusedPlan* d_fp, const uint8_t* d_sender, uint64_t* partials);

@@ -57,6 +57,20 @@ __device__ __forceinline__ void leaf_block(uint32_t me, uint64_t seed, uint64_t 
     static_for<0, S>([&](auto b) { R[b()] = cnt[b()].ge(S / 2 + 1); });  // inner tie -> non-attack
 }
 
+// Bit-sliced count of one matrix column in an LDS word image: the direct value
+// img[diag] plus the child results of rows a != b of prefix sr (s members).
+template <int P>
+__device__ __forceinline__ Count<P> column_count(const uint64_t* img, uint32_t diag,
+                                                 uint32_t child, uint32_t sr, uint32_t s,
+                                                 uint32_t b) {
+    Count<P> cnt;
+    cnt.add(img[diag]);
+    const uint32_t base = child + sr * s * (s - 1);
+    for (uint32_t a = 0; a < b; ++a) cnt.add(img[base + a * (s - 1) + b - 1]);
+    for (uint32_t a = b + 1; a < s; ++a) cnt.add(img[base + a * (s - 1) + b]);
+    return cnt;
+}
+
 // ---------------------------------------------------------------------------
 // LEVELS: one thread per (leaf block, word)
 // ---------------------------------------------------------------------------
@@ -65,17 +79,18 @@ __global__ __launch_bounds__(256) void k_leaf(uint32_t me, uint64_t seed, uint64
                                               FastDiv divW, uint32_t work,
                                               const uint64_t* __restrict__ Lm1,
                                               const uint64_t* __restrict__ F,
-                                              const uint8_t* __restrict__ snd_m1,
+                                              const uint64_t* __restrict__ members,
                                               uint64_t* __restrict__ Rm1) {
     const uint32_t W = divW.d;
     for (uint32_t idx = blockIdx.x * 256 + threadIdx.x; idx < work; idx += gridDim.x * 256) {
         const uint32_t sr = fdiv(idx, divW);
         const uint32_t w = idx - sr * W;
+        const uint64_t mem = members[sr];  // S member ids, 5 bits each
         uint64_t diag[S], Fm[S], R[S];
         static_for<0, S>([&](auto a) {
             const uint64_t x = (uint64_t)sr * S + a();
             diag[a()] = Lm1[x * W + w];
-            Fm[a()] = F[(uint64_t)snd_m1[x] * W + w];
+            Fm[a()] = F[((mem >> (5 * a())) & 31u) * W + w];
         });
         leaf_block<S>(me, seed, gw0 + w, sr, diag, Fm, R);
         static_for<0, S>([&](auto b) { Rm1[((uint64_t)sr * S + b()) * W + w] = R[b()]; });
@@ -94,7 +109,8 @@ template <int S>
 __global__ __launch_bounds__(kFusedThreads, (S <= 7 ? 4 : 2)) void k_fused(
     const FusedPlan* __restrict__ fpp, uint64_t seed, GenSpec gs, uint64_t first_trial,
     uint64_t batch, const uint32_t* __restrict__ faulty, const uint8_t* __restrict__ order,
-    const uint8_t* __restrict__ sender, uint64_t* __restrict__ decisions,
+    const uint8_t* __restrict__ sender, const uint64_t* __restrict__ members,
+    uint64_t* __restrict__ decisions,
     uint8_t* __restrict__ outcome, uint64_t* __restrict__ partial) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     // run counters live in LDS (not in registers across the leaf stage)
@@ -174,12 +190,12 @@ __global__ __launch_bounds__(kFusedThreads, (S <= 7 ? 4 : 2)) void k_fused(
                 uint64_t* img = lds + (uint64_t)lw * stride;
                 const uint64_t gw = gwg + lw;
                 const uint32_t x0 = sr * S;
-                const uint32_t snd1 = fp.snd_off[me - 1] + x0;
+                const uint64_t mem = members[sr];  // S member ids, 5 bits each
                 const uint32_t offR = fp.offR[me - 1] + x0;  // L_{me-1}[sigma.*], then R_{me-1}
                 uint64_t diag[S], Fm[S], R[S];
                 static_for<0, S>([&](auto a) {
                     diag[a()] = img[offR + a()];
-                    Fm[a()] = img[sender[snd1 + a()]];
+                    Fm[a()] = img[(mem >> (5 * a())) & 31u];
                 });
                 leaf_block<S>(me, seed, gw, sr, diag, Fm, R);
                 static_for<0, S>([&](auto b) { img[offR + b()] = R[b()]; });
@@ -193,13 +209,10 @@ __global__ __launch_bounds__(kFusedThreads, (S <= 7 ? 4 : 2)) void k_fused(
                 const uint32_t lw = it / Sp, y = it - lw * Sp;
                 uint64_t* img = lds + (uint64_t)lw * stride;
                 const uint32_t sr = y / s, b = y - sr * s;
-                Count<5> cnt;
-                cnt.add(img[fp.offL[p] + y]);
-                for (uint32_t a = 0; a < s; ++a) {
-                    if (a == b) continue;
-                    cnt.add(img[fp.offR[p + 1] + (sr * s + a) * (s - 1) + (b - (b > a))]);
-                }
-                img[fp.offR[p] + y] = cnt.ge(thr);
+                const uint32_t d = fp.offL[p] + y, c = fp.offR[p + 1];
+                img[fp.offR[p] + y] = s < 8    ? column_count<3>(img, d, c, sr, s, b).ge(thr)
+                                      : s < 16 ? column_count<4>(img, d, c, sr, s, b).ge(thr)
+                                               : column_count<5>(img, d, c, sr, s, b).ge(thr);
             }
             __syncthreads();
         }
@@ -208,14 +221,16 @@ __global__ __launch_bounds__(kFusedThreads, (S <= 7 ? 4 : 2)) void k_fused(
         for (uint32_t it = tid; it < L * WPB; it += T) {
             const uint32_t lw = it / L, b = it - lw * L;
             uint64_t* img = lds + (uint64_t)lw * stride;
-            Count<5> cnt;
-            cnt.add(img[fp.offL[0] + b]);
-            for (uint32_t a = 0; a < L; ++a) {
-                if (a == b) continue;
-                cnt.add(img[fp.offR[1] + a * (L - 1) + (b - (b > a))]);
+            uint64_t att, tie;
+            if (L < 16) {
+                const Count<4> cnt = column_count<4>(img, fp.offL[0] + b, fp.offR[1], 0, L, b);
+                att = cnt.ge(L / 2 + 1);
+                tie = (L & 1u) ? 0ull : (cnt.ge(L / 2) & ~att);
+            } else {
+                const Count<5> cnt = column_count<5>(img, fp.offL[0] + b, fp.offR[1], 0, L, b);
+                att = cnt.ge(L / 2 + 1);
+                tie = (L & 1u) ? 0ull : (cnt.ge(L / 2) & ~att);
             }
-            const uint64_t att = cnt.ge(L / 2 + 1);
-            const uint64_t tie = (L & 1u) ? 0ull : (cnt.ge(L / 2) & ~att);
             // stash after the word image's live data: use the R_{me-1} region
             img[fp.offRoot + b] = att;
             img[fp.offRoot + L + b] = tie;
@@ -225,30 +240,21 @@ __global__ __launch_bounds__(kFusedThreads, (S <= 7 ? 4 : 2)) void k_fused(
             const uint64_t* img = lds + (uint64_t)lw * stride;
             const uint64_t w = w0 + lw;
             const uint64_t i = w * 64 + lane;
-            TrialCounts tc;
-            if (w < total_words && ((img[n + 2] >> lane) & 1ull)) {
-                uint32_t A = 0, U = 0, fm = 0;
-                for (uint32_t b = 0; b < L; ++b) {
-                    A |= (uint32_t)((img[fp.offRoot + b] >> lane) & 1ull) << (b + 1);
-                    U |= (uint32_t)((img[fp.offRoot + L + b] >> lane) & 1ull) << (b + 1);
-                }
-                for (uint32_t g = 0; g < n; ++g) fm |= (uint32_t)((img[g] >> lane) & 1ull) << g;
-                const uint32_t ob = (uint32_t)(img[n] >> lane) & 1u;
-                const uint32_t oo = (uint32_t)(img[n + 1] >> lane) & 1u;
-                uint64_t dec;
-                uint32_t out;
-                finish_trial(n, me, fm, oo ? 2u : ob, A, U, dec, out, tc);
-                if (decisions) decisions[i] = dec;
-                if (outcome) outcome[i] = (uint8_t)out;
+            const bool live = w < total_words && ((img[n + 2] >> lane) & 1ull);
+            uint32_t A = 0, U = 0, fm = 0;
+            for (uint32_t b = 0; b < L; ++b) {
+                A |= (uint32_t)((img[fp.offRoot + b] >> lane) & 1ull) << (b + 1);
+                U |= (uint32_t)((img[fp.offRoot + L + b] >> lane) & 1ull) << (b + 1);
             }
-            // wave sum, then one LDS atomic per counter (integer: order-free)
-#pragma unroll
-            for (int c = 0; c < C_NUM; ++c) {
-                uint32_t x = tc.v[c];
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-                if (lane == 0 && x) atomicAdd(&blockcnt[c], (unsigned long long)x);
+            for (uint32_t g = 0; g < n; ++g) fm |= (uint32_t)((img[g] >> lane) & 1ull) << g;
+            const uint32_t ob = (uint32_t)(img[n] >> lane) & 1u;
+            const uint32_t oo = (uint32_t)(img[n + 1] >> lane) & 1u;
+            const TrialResult r = trial_result(n, me, fm, oo ? 2u : ob, A, U);
+            if (live) {
+                if (decisions) decisions[i] = r.dec;
+                if (outcome) outcome[i] = (uint8_t)r.out;
             }
+            wave_counts_add(live, r, blockcnt);  // ballots: one LDS add per counter per wave
         }
         __syncthreads();
     }
@@ -265,7 +271,7 @@ bool leaf_supported(const Geometry& g) {
 
 template <int S>
 static void launch_leaf_s(uint32_t me, uint64_t seed, uint64_t gw0, uint32_t W, uint32_t work,
-                          const uint64_t* Lm1, const uint64_t* F, const uint8_t* snd,
+                          const uint64_t* Lm1, const uint64_t* F, const uint64_t* snd,
                           uint64_t* Rm1, hipStream_t st) {
     uint64_t b = (work + 255) / 256;
     if (b > 16384) b = 16384;
@@ -275,12 +281,12 @@ static void launch_leaf_s(uint32_t me, uint64_t seed, uint64_t gw0, uint32_t W, 
 }
 
 hipError_t launch_leaf(const Geometry& g, uint64_t seed, uint64_t gw0, uint32_t W,
-                       const uint64_t* Lm1, const uint64_t* F, const uint8_t* d_sender,
+                       const uint64_t* Lm1, const uint64_t* F, const uint64_t* d_members,
                        uint64_t* Rm1, hipStream_t st, Prof* prof) {
     ProfScope ps(prof, "k_leaf", st);
     const uint32_t S = g.n - g.me;
     const uint32_t work = (uint32_t)(g.S[g.me - 2] * W);
-    const uint8_t* snd = d_sender + g.sender_off[g.me - 1];
+    const uint64_t* snd = d_members;
     switch (S) {
 #define LEAF_CASE(s) \
     case s: launch_leaf_s<s>(g.me, seed, gw0, W, work, Lm1, F, snd, Rm1, st); break;
@@ -343,7 +349,7 @@ template <int S>
 static void launch_fused_s(const FusedPlan& fp, const FusedPlan* d_fp, uint32_t blocks,
                            const RunArgs& a, const uint8_t* d_sender, uint64_t* partials) {
     hipLaunchKernelGGL(k_fused<S>, dim3(blocks), dim3(fp.threads), fp.lds_bytes, a.stream, d_fp,
-                       a.seed, a.gen, a.first_trial, a.batch, a.faulty, a.order, d_sender,
+                       a.seed, a.gen, a.first_trial, a.batch, a.faulty, a.order, d_sender, a.members,
                        a.decisions, a.outcome, partials);
 }
 

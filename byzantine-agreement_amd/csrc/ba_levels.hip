@@ -332,7 +332,7 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
     }
     if (lay.leaf_fused) {  // L_me generated on the fly: R_{me-1} straight from L_{me-1}
         e = launch_leaf(g, a.seed, gw0, (uint32_t)W, scratch + lay.Lk[g.me - 1], scratch + lay.F,
-                        d_sender, scratch + lay.Rp[g.me - 1], st, a.prof);
+                        a.members, scratch + lay.Rp[g.me - 1], st, a.prof);
         if (e != hipSuccess) return e;
     }
     // inner majorities, bottom-up (levels me-1..1, or me-2..1 after k_leaf)

@@ -1,7 +1,8 @@
 #!/bin/bash
 # GPU-box session: every GPU step has its own time limit; a fault, abort or
 # timeout ends the session (no retries).  Logs land in gpurun_out/.
-# usage: tools/gpu_session.sh [tests] [smoke] [bench] [prof] [pmc]
+# usage: tools/gpu_session.sh [stage ...]
+#   tests smoke bench bench_levels bench_fused prof pmc philox
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -13,10 +14,17 @@ run() {  # name seconds cmd...
   timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
   echo "[$(date +%T)] $name rc=$rc" | tee -a gpurun_out/steps.log
-  tail -5 "gpurun_out/$name.log"
+  tail -3 "gpurun_out/$name.log"
   return $rc
 }
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }  # 1 = ordinary test failure
+BENCH_PMC="$ROOT/bench.py --steps 3 --warmup 1 --no-cpu --no-profile"
+pmc_pass() {  # name counters...
+  local name=$1; shift
+  (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv \
+     -d "$ROOT/gpurun_out/pmc" -o "$name" -- python3 $BENCH_PMC > "$ROOT/gpurun_out/pmc_$name.log" 2>&1)
+  local rc=$?; echo "pmc $name rc=$rc" | tee -a gpurun_out/steps.log; return $rc
+}
 for s in $STAGES; do
   case $s in
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
@@ -24,10 +32,15 @@ for s in $STAGES; do
     bench) run bench 600 python -u bench.py --steps 20 --warmup 3 || exit $? ;;
     bench_levels) run bench_levels 600 python -u bench.py --steps 20 --warmup 3 --engine levels --no-cpu || exit $? ;;
     bench_fused) run bench_fused 600 python -u bench.py --steps 20 --warmup 3 --engine fused --no-cpu || exit $? ;;
-    prof) (cd /tmp && export TMPDIR=/tmp && run_dir="$ROOT/gpurun_out/prof" && mkdir -p "$run_dir" && \
-           timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$run_dir" -o run -- \
+    philox) run philox 120 ./tools/philox_bench || exit $? ;;
+    prof) (cd /tmp && export TMPDIR=/tmp && mkdir -p "$ROOT/gpurun_out/prof" && \
+           timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/prof" -o run -- \
              python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu --no-profile > "$ROOT/gpurun_out/prof.log" 2>&1); rc=$?
           echo "prof rc=$rc" | tee -a gpurun_out/steps.log; tail -3 gpurun_out/prof.log; [ $rc -eq 0 ] || exit $rc ;;
+    pmc) pmc_pass sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY || exit $?
+         pmc_pass fetch FETCH_SIZE GRBM_GUI_ACTIVE GRBM_COUNT || exit $?
+         pmc_pass write WRITE_SIZE || exit $?
+         pmc_pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR || exit $? ;;
     *) echo "unknown stage $s"; exit 2 ;;
   esac
 done
