@@ -179,6 +179,7 @@ struct ProfTotal {
 
 struct ba_ctx {
     int device = 0;
+    uint32_t cu_count = 256;
     hipStream_t stream = nullptr;
     size_t scratch_budget = 8ull << 30;
     bool leaf_fusion = true;  // LEVELS uses k_leaf when available (BA_NO_LEAF_FUSION=1: off)
@@ -272,6 +273,10 @@ extern "C" int ba_ctx_create(int device, ba_ctx** out) {
     HIP_TRY(hipSetDevice(device));
     auto* ctx = new ba_ctx();
     ctx->device = device;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+        cus > 0)
+        ctx->cu_count = (uint32_t)cus;
     if (const char* s = getenv("BA_SCRATCH_BYTES")) ctx->scratch_budget = strtoull(s, nullptr, 0);
     if (const char* s = getenv("BA_NO_LEAF_FUSION")) ctx->leaf_fusion = strcmp(s, "1") != 0;
     hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
@@ -444,6 +449,7 @@ extern "C" int ba_run_trials_device(ba_ctx* ctx, const ba_params* p, uint64_t ba
     if (!ge) return rc;
     const Geometry& g = ge->g;
     a.members = (const uint64_t*)ge->members.p;
+    a.cu_count = ctx->cu_count;
     const bool fused_ok = ge->fused_ok;
     if (p->engine == BA_ENGINE_FUSED && !fused_ok)
         return fail(BA_ENOTSUP, "FUSED engine needs 2 <= m_eff <= %d and n - m_eff <= %d with the "

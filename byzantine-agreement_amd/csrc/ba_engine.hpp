@@ -45,6 +45,7 @@ struct RunArgs {
     hipStream_t stream = nullptr;
     Prof* prof = nullptr;
     const uint64_t* members = nullptr;  // device copy of Geometry::members
+    uint32_t cu_count = 256;            // compute units of the ctx device
 };
 
 struct ProfScope {  // RAII: times one launch when profiling is on

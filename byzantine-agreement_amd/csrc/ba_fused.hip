@@ -121,11 +121,16 @@ __global__ __launch_bounds__(kFusedThreads, (S <= 7 ? 4 : 2)) void k_fused(
     const uint32_t stride = fp.word_stride;  // uint64 words per trial word in LDS
     if (tid < 16) blockcnt[tid] = 0;
     const uint64_t total_words = (batch + 63) / 64;
-    const uint64_t groups = (total_words + WPB - 1) / WPB;
-    for (uint64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
-        const uint64_t w0 = grp * WPB;  // first word of this group (call-relative)
+    // balanced persistent grid: block b owns a contiguous run of words, taken
+    // in groups of at most WPB (the grid is one block per resident slot, so a
+    // partial last round of groups never idles most of the chip)
+    const uint64_t per_block = (total_words + gridDim.x - 1) / gridDim.x;
+    const uint64_t wbeg = (uint64_t)blockIdx.x * per_block;
+    const uint64_t wend = wbeg + per_block < total_words ? wbeg + per_block : total_words;
+    for (uint64_t w0 = wbeg; w0 < wend; w0 += WPB) {
+        const uint32_t nw = (uint32_t)(wend - w0 < WPB ? wend - w0 : WPB);  // words this group
         // ---- A: inputs -> bit-sliced words (one wave per word) -----------------
-        for (uint32_t lw = wv; lw < WPB; lw += T / 64) {
+        for (uint32_t lw = wv; lw < nw; lw += T / 64) {
             uint64_t* img = lds + (uint64_t)lw * stride;
             const uint64_t i = (w0 + lw) * 64 + lane;
             const bool valid = (w0 + lw) < total_words && i < batch;
@@ -158,12 +163,10 @@ __global__ __launch_bounds__(kFusedThreads, (S <= 7 ? 4 : 2)) void k_fused(
         // exactly those S words with its S majorities.
         for (uint32_t k = 0; k + 1 <= me; ++k) {
             const uint32_t outk = (k + 1 == me) ? fp.offR[me - 1] : fp.offL[k];
-            const uint32_t Sk = fp.S[k], npair = (Sk + 1) / 2;
-            for (uint32_t it = tid; it < npair * WPB; it += T) {
-                const uint32_t lw = it / npair, pair = it - lw * npair;
+            const uint32_t Sk = fp.S[k], npair = (Sk + 1) / 2, items = npair * nw;
+            auto relay = [&](uint32_t item, uint64_t lie0, uint64_t lie1) {
+                const uint32_t lw = item / npair, pair = item - lw * npair;
                 uint64_t* img = lds + (uint64_t)lw * stride;
-                uint64_t lie0, lie1;
-                lie_pair(seed, k, pair, gwg + lw, lie0, lie1);
                 static_for<0, 2>([&](auto h) {
                     const uint32_t x = 2 * pair + h();
                     if (x >= Sk) return;
@@ -179,13 +182,23 @@ __global__ __launch_bounds__(kFusedThreads, (S <= 7 ? 4 : 2)) void k_fused(
                     const uint64_t lie = h() ? lie1 : lie0;
                     img[outk + x] = (fw & lie) | (~fw & parent);
                 });
+            };
+            // two items per thread per pass: two independent Philox chains in flight
+            for (uint32_t it = tid; it < items; it += 2 * T) {
+                const uint32_t it2 = it + T < items ? it + T : it;
+                const uint32_t lwa = it / npair, lwb = it2 / npair;
+                uint64_t a0, a1, b0, b1;
+                lie_pair(seed, k, it - lwa * npair, gwg + lwa, a0, a1);
+                lie_pair(seed, k, it2 - lwb * npair, gwg + lwb, b0, b1);
+                relay(it, a0, a1);
+                if (it2 != it) relay(it2, b0, b1);
             }
             __syncthreads();
         }
         // ---- C: leaf blocks (sigma at level me-2), R_{me-1} into LDS -------------
         {
             const uint32_t Q = fp.S[me - 2];
-            for (uint32_t it = tid; it < Q * WPB; it += T) {
+            for (uint32_t it = tid; it < Q * nw; it += T) {
                 const uint32_t lw = it / Q, sr = it - lw * Q;
                 uint64_t* img = lds + (uint64_t)lw * stride;
                 const uint64_t gw = gwg + lw;
@@ -205,7 +218,7 @@ __global__ __launch_bounds__(kFusedThreads, (S <= 7 ? 4 : 2)) void k_fused(
         // ---- D: inner majorities p = me-2 .. 1 ----------------------------------
         for (int p = (int)me - 2; p >= 1; --p) {
             const uint32_t Sp = fp.S[p], s = L - (uint32_t)p, thr = s / 2 + 1;
-            for (uint32_t it = tid; it < Sp * WPB; it += T) {
+            for (uint32_t it = tid; it < Sp * nw; it += T) {
                 const uint32_t lw = it / Sp, y = it - lw * Sp;
                 uint64_t* img = lds + (uint64_t)lw * stride;
                 const uint32_t sr = y / s, b = y - sr * s;
@@ -218,7 +231,7 @@ __global__ __launch_bounds__(kFusedThreads, (S <= 7 ? 4 : 2)) void k_fused(
         }
         // ---- E: root majority (tie -> undefined) + per-trial epilogue -----------
         // roots go to the (now dead) R_{me-1} area: A at +0, U at +L
-        for (uint32_t it = tid; it < L * WPB; it += T) {
+        for (uint32_t it = tid; it < L * nw; it += T) {
             const uint32_t lw = it / L, b = it - lw * L;
             uint64_t* img = lds + (uint64_t)lw * stride;
             uint64_t att, tie;
@@ -236,7 +249,7 @@ __global__ __launch_bounds__(kFusedThreads, (S <= 7 ? 4 : 2)) void k_fused(
             img[fp.offRoot + L + b] = tie;
         }
         __syncthreads();
-        for (uint32_t lw = wv; lw < WPB; lw += T / 64) {
+        for (uint32_t lw = wv; lw < nw; lw += T / 64) {
             const uint64_t* img = lds + (uint64_t)lw * stride;
             const uint64_t w = w0 + lw;
             const uint64_t i = w * 64 + lane;
@@ -356,8 +369,20 @@ static void launch_fused_s(const FusedPlan& fp, const FusedPlan* d_fp, uint32_t 
 hipError_t launch_fused(const RunArgs& a, const Geometry& g, const FusedPlan& fp,
                         const FusedPlan* d_fp, const uint8_t* d_sender, uint64_t* partials) {
     const uint64_t words = (a.batch + 63) / 64;
-    const uint64_t groups = (words + fp.wpb - 1) / fp.wpb;
-    const uint32_t blocks = (uint32_t)(groups < (uint64_t)kPartialRows ? groups : kPartialRows);
+    // one block per resident slot (occupancy x CUs): each owns an equal run of words
+    int occ = 0;
+    switch (g.n - g.me) {
+#define OCC_CASE(s) \
+    case s: (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_fused<s>, fp.threads, fp.lds_bytes); break;
+        OCC_CASE(2) OCC_CASE(3) OCC_CASE(4) OCC_CASE(5) OCC_CASE(6) OCC_CASE(7)
+        OCC_CASE(8) OCC_CASE(9) OCC_CASE(10) OCC_CASE(11) OCC_CASE(12)
+#undef OCC_CASE
+        default: return hipErrorInvalidValue;
+    }
+    if (occ < 1) occ = 1;
+    uint64_t slots = (uint64_t)occ * a.cu_count;
+    if (slots > (uint64_t)kPartialRows) slots = kPartialRows;
+    const uint32_t blocks = (uint32_t)(words < slots ? words : slots);
     {
         ProfScope ps(a.prof, "k_fused", a.stream);
         switch (g.n - g.me) {
