@@ -33,7 +33,8 @@ COUNTER_NAMES = ["trials", "agreement", "validity_applicable", "validity", "quor
                  "bound_violations", "faulty_total", "attack_decisions"]
 EXPORTS = ["ba_version", "ba_device_count", "ba_ctx_create", "ba_ctx_destroy", "ba_last_error",
            "ba_run_trials", "ba_run_trials_device", "ba_tree_slots", "ba_level_slots",
-           "ba_engine_for", "ba_profile_enable", "ba_profile_read"]
+           "ba_engine_for", "ba_profile_enable", "ba_profile_read", "ba_mt_seed", "ba_mt_next32",
+           "ba_om1_coin_count", "ba_mt_draw_coins", "ba_mt_table"]
 
 
 class BAError(RuntimeError):
@@ -49,6 +50,11 @@ class Params(ctypes.Structure):
                 ("order_value", ctypes.c_uint32), ("engine", ctypes.c_uint32),
                 ("first_trial", ctypes.c_uint64), ("table_stride", ctypes.c_uint32),
                 ("reserved", ctypes.c_uint32 * 5)]
+
+
+class MTState(ctypes.Structure):
+    """ba_mt: CPython-compatible MT19937 state (include/ba.h)."""
+    _fields_ = [("state", ctypes.c_uint32 * 624), ("index", ctypes.c_uint32)]
 
 
 class Counters(ctypes.Structure):
@@ -96,6 +102,14 @@ def load(path: str | None = None):
     lib.ba_profile_enable.argtypes = [vp, i32]
     lib.ba_profile_read.argtypes = [vp, i32, ctypes.c_char_p, i32, ctypes.POINTER(u64),
                                     ctypes.POINTER(ctypes.c_double)]
+    lib.ba_mt_seed.argtypes = [ctypes.POINTER(MTState), u64]
+    lib.ba_mt_seed.restype = None
+    lib.ba_mt_next32.argtypes = [ctypes.POINTER(MTState)]
+    lib.ba_mt_next32.restype = u32
+    lib.ba_om1_coin_count.argtypes = [u32, u32, u32, u32]
+    lib.ba_om1_coin_count.restype = u32
+    lib.ba_mt_draw_coins.argtypes = [ctypes.POINTER(MTState), u32, vp, u32]
+    lib.ba_mt_table.argtypes = [u32, u32, u64, vp, vp, vp, u32, vp, vp, i32]
     if lib.ba_version() != ABI_VERSION:
         raise RuntimeError(f"libba_hip ABI {lib.ba_version()} != {ABI_VERSION}")
     if path is None:
@@ -214,6 +228,49 @@ class Engine:
             self.handle, ctypes.byref(params), batch, d_faulty or None, d_order or None,
             d_table or None, d_poll or None, d_decisions or None, d_outcome or None,
             d_counters or None, stream or None))
+
+
+class MT:
+    """ba.py's coin source (random.seed / random.randint(0, 1)), host-side C++."""
+
+    def __init__(self, seed: int = 0):
+        self.lib = load()
+        self.st = MTState()
+        self.seed(seed)
+
+    def seed(self, seed: int):
+        if not 0 <= seed < (1 << 64):
+            raise ValueError("seed must be in [0, 2^64)")
+        self.lib.ba_mt_seed(ctypes.byref(self.st), seed)
+
+    def next32(self) -> int:
+        return int(self.lib.ba_mt_next32(ctypes.byref(self.st)))
+
+    def coins(self, count: int, words: int | None = None) -> np.ndarray:
+        """Draw `count` coins (1 = attack) packed into uint32 words."""
+        words = max(1, (count + 31) // 32) if words is None else words
+        buf = np.zeros(words, np.uint32)
+        _check(self.lib, self.lib.ba_mt_draw_coins(ctypes.byref(self.st), count, buf.ctypes.data,
+                                                   words))
+        return buf
+
+
+def om1_coin_count(n: int, m: int, faulty_mask: int, poll: int = 0) -> int:
+    return int(load().ba_om1_coin_count(n, m, faulty_mask, poll))
+
+
+def mt_table(n, m, seeds, faulty, poll=None, threads=0):
+    """Batched ba.py replay table: (table[batch, stride] uint32, next_word[batch] uint32)."""
+    lib = load()
+    seeds = np.ascontiguousarray(seeds, np.uint64)
+    faulty = np.ascontiguousarray(faulty, np.uint32)
+    poll = None if poll is None else np.ascontiguousarray(poll, np.uint32)
+    stride = table_stride(n)
+    tab = np.zeros((len(seeds), stride), np.uint32)
+    nxt = np.zeros(len(seeds), np.uint32)
+    _check(lib, lib.ba_mt_table(n, m, len(seeds), seeds.ctypes.data, faulty.ctypes.data,
+                                _ptr(poll), stride, tab.ctypes.data, nxt.ctypes.data, threads))
+    return tab, nxt
 
 
 def pack_coins(rows, n):

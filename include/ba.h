@@ -168,6 +168,34 @@ int ba_profile_enable(struct ba_ctx* ctx, int on);
 int ba_profile_read(struct ba_ctx* ctx, int index, char* name, int name_len,
                     uint64_t* launches, double* total_ms);
 
+/* ---- ba.py's coin source (host only, no device needed) --------------------
+ * Replaces the unseeded global CPython MT19937 behind random.randint(0, 1)
+ * (ba.py:45 relay lies, ba.py:269 commander lies).  ba_mt_seed(s) equals
+ * random.seed(s) for 0 <= s < 2^64; ba_mt_next32 equals random.getrandbits(32);
+ * each coin is one random.randint(0, 1) draw (1 = "attack", i.e. the draw was
+ * 0).  Coins are packed in BA_LIE_TABLE layout, in ba.py's canonical draw
+ * order, so a table row feeds ba_run_trials directly. */
+typedef struct ba_mt {
+    uint32_t state[624];
+    uint32_t index;
+} ba_mt;
+
+void ba_mt_seed(ba_mt* mt, uint64_t seed);
+uint32_t ba_mt_next32(ba_mt* mt);
+/* coins one ba.py round draws: (n-1) if the commander is faulty (ba.py:263-273),
+ * plus, per lieutenant r, one per other faulty lieutenant and one for a faulty
+ * commander it polls (ba.py:169-186).  m == 0: commander coins only. */
+uint32_t ba_om1_coin_count(uint32_t n, uint32_t m, uint32_t faulty_mask, uint32_t poll_commander);
+/* draw `count` coins into packed[0..words) (zeroed first) */
+int ba_mt_draw_coins(ba_mt* mt, uint32_t count, uint32_t* packed, uint32_t words);
+/* Batched replay table: trial t is random.seed(seeds[t]) followed by one ba.py
+ * round over (faulty_mask[t], poll_commander[t] or 0); row t of `table`
+ * (stride uint32 words) receives its coins; next_word[t] (optional) the next
+ * getrandbits(32) after the round.  threads <= 0: all host cores. */
+int ba_mt_table(uint32_t n, uint32_t m, uint64_t batch, const uint64_t* seeds,
+                const uint32_t* faulty_mask, const uint32_t* poll_commander, uint32_t stride,
+                uint32_t* table, uint32_t* next_word, int threads);
+
 /* Tree geometry helpers (host only, no device needed). */
 uint64_t ba_tree_slots(uint32_t n, uint32_t m);             /* sum_k |L_k|       */
 uint64_t ba_level_slots(uint32_t n, uint32_t m, uint32_t k); /* |L_k|=P(n-1,k+1) */
