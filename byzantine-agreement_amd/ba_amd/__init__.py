@@ -7,6 +7,6 @@ in the HIP kernels of ../csrc; nothing here computes a decision on the CPU.
 from .lib import (ATTACK, ENGINE_AUTO, ENGINE_FUSED, ENGINE_LEVELS, FAULTY_EXACT,  # noqa: F401
                   FAULTY_GIVEN, FAULTY_RANDOM, LIE_PHILOX, LIE_TABLE, ORDER_CONST,
                   ORDER_GIVEN, ORDER_RANDOM, OTHER, RETREAT, UNDEFINED, BAError, Engine,
-                  RunResult, load)
+                  MT, RunResult, load)
 
-__all__ = ["Engine", "RunResult", "BAError", "load"]
+__all__ = ["Engine", "RunResult", "BAError", "load", "MT"]
