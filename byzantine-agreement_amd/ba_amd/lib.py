@@ -34,7 +34,8 @@ COUNTER_NAMES = ["trials", "agreement", "validity_applicable", "validity", "quor
 EXPORTS = ["ba_version", "ba_device_count", "ba_ctx_create", "ba_ctx_destroy", "ba_last_error",
            "ba_run_trials", "ba_run_trials_device", "ba_tree_slots", "ba_level_slots",
            "ba_engine_for", "ba_profile_enable", "ba_profile_read", "ba_mt_seed", "ba_mt_next32",
-           "ba_om1_coin_count", "ba_mt_draw_coins", "ba_mt_table"]
+           "ba_om1_coin_count", "ba_mt_draw_coins", "ba_mt_table", "ba_vote_slots",
+           "ba_subtree_votes_device", "ba_root_from_votes_device"]
 
 
 class BAError(RuntimeError):
@@ -110,6 +111,12 @@ def load(path: str | None = None):
     lib.ba_om1_coin_count.restype = u32
     lib.ba_mt_draw_coins.argtypes = [ctypes.POINTER(MTState), u32, vp, u32]
     lib.ba_mt_table.argtypes = [u32, u32, u64, vp, vp, vp, u32, vp, vp, i32]
+    lib.ba_vote_slots.argtypes = [u32, u32, u32, u32]
+    lib.ba_vote_slots.restype = u64
+    lib.ba_subtree_votes_device.argtypes = [vp, ctypes.POINTER(Params), u64, u32, u32, vp, vp, vp,
+                                            vp]
+    lib.ba_root_from_votes_device.argtypes = [vp, ctypes.POINTER(Params), u64, vp, vp, vp, vp, vp,
+                                              vp, vp]
     if lib.ba_version() != ABI_VERSION:
         raise RuntimeError(f"libba_hip ABI {lib.ba_version()} != {ABI_VERSION}")
     if path is None:
@@ -229,6 +236,20 @@ class Engine:
             d_table or None, d_poll or None, d_decisions or None, d_outcome or None,
             d_counters or None, stream or None))
 
+    def subtree_votes_device(self, params: Params, batch: int, j_begin: int, j_end: int,
+                             d_votes: int, d_faulty=0, d_order=0, stream=0):
+        """Level-1 child results of first-hop subtrees [j_begin, j_end)."""
+        _check(self.lib, self.lib.ba_subtree_votes_device(
+            self.handle, ctypes.byref(params), batch, j_begin, j_end, d_faulty or None,
+            d_order or None, d_votes, stream or None))
+
+    def root_from_votes_device(self, params: Params, batch: int, d_votes: int, d_counters: int,
+                               d_faulty=0, d_order=0, d_decisions=0, d_outcome=0, stream=0):
+        """Root majorities + quorum from the gathered votes of every subtree."""
+        _check(self.lib, self.lib.ba_root_from_votes_device(
+            self.handle, ctypes.byref(params), batch, d_faulty or None, d_order or None, d_votes,
+            d_decisions or None, d_outcome or None, d_counters, stream or None))
+
 
 class MT:
     """ba.py's coin source (random.seed / random.randint(0, 1)), host-side C++."""
@@ -271,6 +292,11 @@ def mt_table(n, m, seeds, faulty, poll=None, threads=0):
     _check(lib, lib.ba_mt_table(n, m, len(seeds), seeds.ctypes.data, faulty.ctypes.data,
                                 _ptr(poll), stride, tab.ctypes.data, nxt.ctypes.data, threads))
     return tab, nxt
+
+
+def vote_slots(n: int, m: int, j_begin: int, j_end: int) -> int:
+    """Vote slots of first-hop subtrees [j_begin, j_end) per 64-trial word."""
+    return int(load().ba_vote_slots(n, m, j_begin, j_end))
 
 
 def pack_coins(rows, n):

@@ -118,9 +118,22 @@ bool Geometry::build(uint32_t n_, uint32_t me_, uint64_t max_level_slots) {
     return true;
 }
 
-void LevelsLayout::plan(const Geometry& g, uint64_t W_, bool leaf) {
+void LevelsLayout::plan(const Geometry& g, uint64_t W_, bool leaf, uint32_t jb_, uint32_t je_) {
     W = W_;
+    jb = jb_;
+    je = je_;
     leaf_fused = leaf;
+    base.assign(g.me + 1, 0);
+    cnt.assign(g.me + 1, 0);
+    for (uint32_t k = 0; k <= g.me; ++k) {
+        if (k == 0) {
+            cnt[k] = g.S[0];
+        } else {
+            const uint64_t q = g.S[k] / g.L;  // slots per first-hop subtree
+            base[k] = (uint64_t)jb * q;
+            cnt[k] = (uint64_t)(je - jb) * q;
+        }
+    }
     uint64_t o = 0;
     F = o; o += (uint64_t)g.n * W;
     OB = o; o += W;
@@ -130,11 +143,17 @@ void LevelsLayout::plan(const Geometry& g, uint64_t W_, bool leaf) {
     for (uint32_t k = 0; k <= g.me; ++k) {
         if (leaf && k == g.me) break;  // generated on the fly by k_leaf
         Lk[k] = o;
-        o += g.S[k] * W;
+        o += cnt[k] * W;
     }
     Rp.assign(g.me + 1, 0);
-    for (uint32_t p = 1; p < g.me; ++p) { Rp[p] = o; o += g.S[p] * W; }
+    for (uint32_t p = 1; p < g.me; ++p) { Rp[p] = o; o += cnt[p] * W; }
     total = o;
+}
+
+uint64_t LevelsLayout::words_per_trial_word(const Geometry& g, bool leaf, uint32_t jb, uint32_t je) {
+    LevelsLayout l;
+    l.plan(g, 1, leaf, jb, je);
+    return l.total;
 }
 }  // namespace ba
 
@@ -403,20 +422,12 @@ static GeoEntry* geometry(ba_ctx* ctx, uint32_t n, uint32_t me, int* rc) {
 }
 
 // ---------------------------------------------------------------------------
-// device entry point
+// device entry points
 // ---------------------------------------------------------------------------
-extern "C" int ba_run_trials_device(ba_ctx* ctx, const ba_params* p, uint64_t batch,
-                                    const uint32_t* d_faulty, const uint8_t* d_order,
-                                    const uint32_t* d_table, const uint32_t* d_poll,
-                                    uint64_t* d_decisions, uint8_t* d_outcome,
-                                    uint64_t* d_counters, void* stream) {
-    if (!ctx) return fail(BA_EINVAL, "ctx is NULL");
-    int rc = validate(p, batch, d_faulty != nullptr, d_order != nullptr, d_table != nullptr);
-    if (rc != BA_OK) return rc;
-    if (!d_counters) return fail(BA_EINVAL, "d_counters is required on the device path");
-    if (batch == 0) return BA_OK;
-    HIP_TRY(hipSetDevice(ctx->device));
-
+static RunArgs make_args(ba_ctx* ctx, const ba_params* p, uint64_t batch, const uint32_t* d_faulty,
+                         const uint8_t* d_order, const uint32_t* d_table, const uint32_t* d_poll,
+                         uint64_t* d_decisions, uint8_t* d_outcome, uint64_t* d_counters,
+                         void* stream) {
     RunArgs a;
     a.n = p->n;
     a.m = p->m;
@@ -436,7 +447,58 @@ extern "C" int ba_run_trials_device(ba_ctx* ctx, const ba_params* p, uint64_t ba
     a.counters = d_counters;
     a.stream = stream ? (hipStream_t)stream : ctx->stream;
     a.prof = &ctx->prof;
+    a.cu_count = ctx->cu_count;
+    return a;
+}
 
+// LEVELS over the first-hop subtrees [jb, je): chunk the batch so the scratch
+// fits the budget and 32-bit indices hold.  `whole` = one chunk or BA_ETOOBIG
+// (the subtree/vote entry points keep one vote stride for the whole batch).
+static int run_levels(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge, const LevelsJob& job,
+                      uint32_t jb, uint32_t je, bool whole, uint64_t* partials) {
+    const Geometry& g = ge->g;
+    const bool leaf = ctx->leaf_fusion && leaf_supported(g);
+    const uint64_t per_word = LevelsLayout::words_per_trial_word(g, leaf, jb, je) * sizeof(uint64_t);
+    uint64_t max_level = 0;
+    for (uint64_t s : g.S) max_level = s > max_level ? s : max_level;
+    const uint64_t words = (a.batch + 63) / 64;
+    uint64_t chunk = ctx->scratch_budget / per_word;
+    const uint64_t idx_cap = (1ull << 31) / (max_level + 1);
+    if (chunk > idx_cap) chunk = idx_cap;
+    if (chunk > words) chunk = words;
+    if (chunk == 0 || (whole && chunk < words))
+        return fail(BA_ETOOBIG, "%llu 64-trial words need %llu bytes of scratch each (budget %zu%s)",
+                    (unsigned long long)words, (unsigned long long)per_word, ctx->scratch_budget,
+                    whole ? ", one chunk required: split the batch" : "");
+    LevelsLayout lay;
+    lay.plan(g, chunk, leaf, jb, je);
+    int rc;
+    if ((rc = ctx->scratch.grow(lay.total * sizeof(uint64_t))) != BA_OK) return rc;
+    for (uint64_t w0 = 0; w0 < words; w0 += chunk) {
+        const uint64_t wn = (words - w0) < chunk ? (words - w0) : chunk;
+        const uint64_t trial0 = w0 * 64;
+        const uint64_t nt = (a.batch - trial0) < wn * 64 ? (a.batch - trial0) : wn * 64;
+        LevelsLayout cl;
+        cl.plan(g, wn, leaf, jb, je);
+        HIP_TRY(launch_levels_chunk(a, g, (const uint8_t*)ge->sender.p, (uint64_t*)ctx->scratch.p,
+                                    cl, trial0, nt, partials, job));
+    }
+    return BA_OK;
+}
+
+extern "C" int ba_run_trials_device(ba_ctx* ctx, const ba_params* p, uint64_t batch,
+                                    const uint32_t* d_faulty, const uint8_t* d_order,
+                                    const uint32_t* d_table, const uint32_t* d_poll,
+                                    uint64_t* d_decisions, uint8_t* d_outcome,
+                                    uint64_t* d_counters, void* stream) {
+    if (!ctx) return fail(BA_EINVAL, "ctx is NULL");
+    int rc = validate(p, batch, d_faulty != nullptr, d_order != nullptr, d_table != nullptr);
+    if (rc != BA_OK) return rc;
+    if (!d_counters) return fail(BA_EINVAL, "d_counters is required on the device path");
+    if (batch == 0) return BA_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    RunArgs a = make_args(ctx, p, batch, d_faulty, d_order, d_table, d_poll, d_decisions,
+                          d_outcome, d_counters, stream);
     if ((rc = ctx->partials.grow(sizeof(uint64_t) * 16 * kPartialRows)) != BA_OK) return rc;
     uint64_t* partials = (uint64_t*)ctx->partials.p;
 
@@ -449,7 +511,6 @@ extern "C" int ba_run_trials_device(ba_ctx* ctx, const ba_params* p, uint64_t ba
     if (!ge) return rc;
     const Geometry& g = ge->g;
     a.members = (const uint64_t*)ge->members.p;
-    a.cu_count = ctx->cu_count;
     const bool fused_ok = ge->fused_ok;
     if (p->engine == BA_ENGINE_FUSED && !fused_ok)
         return fail(BA_ENOTSUP, "FUSED engine needs 2 <= m_eff <= %d and n - m_eff <= %d with the "
@@ -460,32 +521,70 @@ extern "C" int ba_run_trials_device(ba_ctx* ctx, const ba_params* p, uint64_t ba
                              (const uint8_t*)ge->sender.p, partials));
         return BA_OK;
     }
-    // LEVELS: chunk the batch so the scratch fits the budget and 32-bit indices hold
-    const bool leaf = ctx->leaf_fusion && leaf_supported(g);
-    const uint64_t per_word = LevelsLayout::words_per_trial_word(g, leaf) * sizeof(uint64_t);
-    uint64_t max_level = 0;
-    for (uint64_t s : g.S) max_level = s > max_level ? s : max_level;
-    uint64_t words = (batch + 63) / 64;
-    uint64_t chunk = ctx->scratch_budget / per_word;
-    const uint64_t idx_cap = (1ull << 31) / (max_level + 1);
-    if (chunk > idx_cap) chunk = idx_cap;
-    if (chunk > words) chunk = words;
-    if (chunk == 0)
-        return fail(BA_ETOOBIG, "one 64-trial word needs %llu bytes of scratch (budget %zu)",
-                    (unsigned long long)per_word, ctx->scratch_budget);
-    LevelsLayout lay;
-    lay.plan(g, chunk, leaf);
-    if ((rc = ctx->scratch.grow(lay.total * sizeof(uint64_t))) != BA_OK) return rc;
-    for (uint64_t w0 = 0; w0 < words; w0 += chunk) {
-        const uint64_t wn = (words - w0) < chunk ? (words - w0) : chunk;
-        const uint64_t trial0 = w0 * 64;
-        const uint64_t nt = (batch - trial0) < wn * 64 ? (batch - trial0) : wn * 64;
-        LevelsLayout cl;
-        cl.plan(g, wn, leaf);
-        HIP_TRY(launch_levels_chunk(a, g, (const uint8_t*)ge->sender.p, (uint64_t*)ctx->scratch.p,
-                                    cl, trial0, nt, partials));
-    }
+    return run_levels(ctx, a, ge, LevelsJob{}, 0, g.L, false, partials);
+}
+
+extern "C" uint64_t ba_vote_slots(uint32_t n, uint32_t m, uint32_t j_begin, uint32_t j_end) {
+    if (n < 3 || n > BA_MAX_GENERALS || effective_depth(n, m) == 0) return 0;
+    if (j_begin > j_end || j_end > n - 1) return 0;
+    return (uint64_t)(j_end - j_begin) * (n - 2);
+}
+
+static int validate_split(ba_ctx* ctx, const ba_params* p, uint64_t batch, const uint32_t* d_faulty,
+                          const uint8_t* d_order) {
+    if (!ctx) return fail(BA_EINVAL, "ctx is NULL");
+    int rc = validate(p, batch, d_faulty != nullptr, d_order != nullptr, false);
+    if (rc != BA_OK) return rc;
+    if (p->lie_mode != BA_LIE_PHILOX)
+        return fail(BA_ENOTSUP, "the first-hop split runs Philox lies only (table mode is OM(1))");
+    if (p->engine == BA_ENGINE_FUSED)
+        return fail(BA_ENOTSUP, "the first-hop split runs on the LEVELS engine");
+    if (effective_depth(p->n, p->m) == 0)
+        return fail(BA_ENOTSUP, "OM(0) has no relay subtrees (n=%u, m=%u)", p->n, p->m);
     return BA_OK;
+}
+
+extern "C" int ba_subtree_votes_device(ba_ctx* ctx, const ba_params* p, uint64_t batch,
+                                       uint32_t j_begin, uint32_t j_end, const uint32_t* d_faulty,
+                                       const uint8_t* d_order, uint64_t* d_votes, void* stream) {
+    int rc = validate_split(ctx, p, batch, d_faulty, d_order);
+    if (rc != BA_OK) return rc;
+    if (j_begin >= j_end || j_end > p->n - 1)
+        return fail(BA_EINVAL, "subtree range [%u, %u) outside [0, %u)", j_begin, j_end, p->n - 1);
+    if (!d_votes) return fail(BA_EINVAL, "d_votes is NULL");
+    if (batch == 0) return BA_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    RunArgs a = make_args(ctx, p, batch, d_faulty, d_order, nullptr, nullptr, nullptr, nullptr,
+                          nullptr, stream);
+    GeoEntry* ge = geometry(ctx, a.n, a.me, &rc);
+    if (!ge) return rc;
+    a.members = (const uint64_t*)ge->members.p;
+    LevelsJob job;
+    job.root = false;
+    job.votes_out = d_votes;
+    return run_levels(ctx, a, ge, job, j_begin, j_end, true, nullptr);
+}
+
+extern "C" int ba_root_from_votes_device(ba_ctx* ctx, const ba_params* p, uint64_t batch,
+                                         const uint32_t* d_faulty, const uint8_t* d_order,
+                                         const uint64_t* d_votes, uint64_t* d_decisions,
+                                         uint8_t* d_outcome, uint64_t* d_counters, void* stream) {
+    int rc = validate_split(ctx, p, batch, d_faulty, d_order);
+    if (rc != BA_OK) return rc;
+    if (!d_votes || !d_counters) return fail(BA_EINVAL, "d_votes and d_counters are required");
+    if (batch == 0) return BA_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    RunArgs a = make_args(ctx, p, batch, d_faulty, d_order, nullptr, nullptr, d_decisions,
+                          d_outcome, d_counters, stream);
+    if ((rc = ctx->partials.grow(sizeof(uint64_t) * 16 * kPartialRows)) != BA_OK) return rc;
+    GeoEntry* ge = geometry(ctx, a.n, a.me, &rc);
+    if (!ge) return rc;
+    a.members = (const uint64_t*)ge->members.p;
+    LevelsJob job;
+    job.tree = false;
+    job.votes_in = d_votes;
+    // an empty subtree range: only the inputs and L_0 are materialised
+    return run_levels(ctx, a, ge, job, 0, 0, true, (uint64_t*)ctx->partials.p);
 }
 
 // ---------------------------------------------------------------------------

@@ -75,16 +75,29 @@ struct Geometry {
 };
 
 // LEVELS engine scratch layout for a chunk of W trial words (uint64 words).
+// A level may be restricted to the first-hop subtrees [jb, je) (SURVEY.md
+// §8e): level k >= 1 then holds global slots [base[k], base[k] + cnt[k]) with
+// base[k] = jb * S[k] / L; level 0 (L slots) is always whole.
 struct LevelsLayout {
     uint64_t W = 0;
+    uint32_t jb = 0, je = 0;
     uint64_t F = 0, OB = 0, OO = 0, VAL = 0;
     std::vector<uint64_t> Lk, Rp;  // Rp[p] valid for 1 <= p < me
+    std::vector<uint64_t> base, cnt;
     uint64_t total = 0;
     bool leaf_fused = false;       // L_me not materialised (k_leaf)
-    void plan(const Geometry& g, uint64_t W, bool leaf);
-    static uint64_t words_per_trial_word(const Geometry& g, bool leaf) {
-        return g.n + 3 + g.slots_total + g.inner_total - (leaf ? g.S[g.me] : 0);
-    }
+    void plan(const Geometry& g, uint64_t W, bool leaf, uint32_t jb, uint32_t je);
+    static uint64_t words_per_trial_word(const Geometry& g, bool leaf, uint32_t jb, uint32_t je);
+};
+
+// What one LEVELS pass computes.  The default is a whole trial batch.  The
+// first-hop split runs `tree` on a subtree range and leaves its level-1 child
+// results (R_1, or L_1 at depth 1) in votes_out; `root` alone reads the
+// gathered votes of every subtree (votes_in) for the root majorities.
+struct LevelsJob {
+    bool tree = true, root = true;
+    uint64_t* votes_out = nullptr;       // [ (je-jb)(L-1) slots ][ W ]
+    const uint64_t* votes_in = nullptr;  // [ L(L-1) slots ][ W ]
 };
 
 constexpr int kPartialRows = 2048;  // max epilogue blocks per launch
@@ -105,15 +118,15 @@ struct FusedPlan {
 bool leaf_supported(const Geometry& g);
 bool plan_fused(const Geometry& g, FusedPlan& fp);
 hipError_t launch_leaf(const Geometry& g, uint64_t seed, uint64_t gw0, uint32_t W,
-                       const uint64_t* Lm1, const uint64_t* F, const uint64_t* d_members,
-                       uint64_t* Rm1, hipStream_t st, Prof* prof);
+                       uint32_t srbase, uint32_t srcnt, const uint64_t* Lm1, const uint64_t* F,
+                       const uint64_t* d_members, uint64_t* Rm1, hipStream_t st, Prof* prof);
 hipError_t launch_fused(const RunArgs& a, const Geometry& g, const FusedPlan& fp,
                         const FusedPlan* d_fp, const uint8_t* d_sender, uint64_t* partials);
 
 hipError_t launch_table(const RunArgs& a, uint64_t* partials);
 hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_t* d_sender,
                                uint64_t* scratch, const LevelsLayout& lay, uint64_t trial0,
-                               uint64_t ntrials, uint64_t* partials);
+                               uint64_t ntrials, uint64_t* partials, const LevelsJob& job);
 hipError_t launch_reduce(const uint64_t* partials, int rows, uint64_t* counters, hipStream_t s,
                          Prof* prof);
 

@@ -56,64 +56,71 @@ __global__ __launch_bounds__(kBlock) void k_input(uint32_t n, uint64_t seed, Gen
 }
 
 // ---------------------------------------------------------------------------
-// relay level k: one thread per (slot pair, word); one Philox call per thread
+// relay level k: one thread per (slot pair, word); one Philox call per thread.
+// Level k holds global slots [xbase, xbase + xcnt) (a first-hop subtree range;
+// the whole level by default), its parent level starts at global slot pbase.
+// Lies stay keyed by the GLOBAL slot pair, so any split gives the same bits.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_relay(uint32_t k, uint32_t S, uint32_t fanout,
-                                                  FastDiv divW, FastDiv divFan, uint32_t work,
-                                                  uint64_t seed, uint64_t gw0,
+__global__ __launch_bounds__(kBlock) void k_relay(uint32_t k, uint32_t xbase, uint32_t xcnt,
+                                                  uint32_t pbase, FastDiv divW, FastDiv divFan,
+                                                  uint32_t work, uint64_t seed, uint64_t gw0,
                                                   const uint64_t* __restrict__ Lprev,
                                                   uint64_t* __restrict__ Lk,
                                                   const uint64_t* __restrict__ F,
                                                   const uint8_t* __restrict__ sender) {
     const uint32_t W = divW.d;
+    const uint32_t pair0 = xbase >> 1, xend = xbase + xcnt;
     for (uint32_t idx = blockIdx.x * kBlock + threadIdx.x; idx < work; idx += grid_threads()) {
-        const uint32_t pair = fdiv(idx, divW);
-        const uint32_t w = idx - pair * W;
+        const uint32_t pl = fdiv(idx, divW);
+        const uint32_t w = idx - pl * W;
+        const uint32_t pair = pair0 + pl;
         uint64_t lie[2];
         lie_pair(seed, k, pair, gw0 + w, lie[0], lie[1]);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const uint32_t x = 2 * pair + h;
-            if (x >= S) break;
+            if (x < xbase || x >= xend) continue;
             uint64_t parent, fw;
             if (k == 0) {  // commander -> lieutenant x (ba.py:263-277)
                 parent = Lprev[w];
                 fw = F[w];
             } else {
                 const uint32_t y = fdiv(x, divFan);
-                parent = Lprev[(uint64_t)y * W + w];
+                parent = Lprev[(uint64_t)(y - pbase) * W + w];
                 fw = F[(uint64_t)sender[y] * W + w];
             }
-            Lk[(uint64_t)x * W + w] = (fw & lie[h]) | (~fw & parent);
+            Lk[(uint64_t)(x - xbase) * W + w] = (fw & lie[h]) | (~fw & parent);
         }
     }
 }
 
 // ---------------------------------------------------------------------------
-// inner majority level p (1 <= p < me): one thread per (slot, word)
+// inner majority level p (1 <= p < me): one thread per (slot, word).  Level p
+// starts at global slot ybase, its child level at cbase (subtree ranges).
 // ---------------------------------------------------------------------------
 template <int P>
 __global__ __launch_bounds__(kBlock) void k_majority(uint32_t s, FastDiv divW, FastDiv divS,
-                                                     uint32_t work,
+                                                     uint32_t work, uint32_t ybase, uint32_t cbase,
                                                      const uint64_t* __restrict__ Lp,
                                                      const uint64_t* __restrict__ C,
                                                      uint64_t* __restrict__ Rp) {
     const uint32_t W = divW.d;
     const uint32_t thr = s / 2 + 1;  // strict majority; inner tie -> non-attack
     for (uint32_t idx = blockIdx.x * kBlock + threadIdx.x; idx < work; idx += grid_threads()) {
-        const uint32_t y = fdiv(idx, divW);
-        const uint32_t w = idx - y * W;
+        const uint32_t yl = fdiv(idx, divW);
+        const uint32_t w = idx - yl * W;
+        const uint32_t y = ybase + yl;
         const uint32_t sr = fdiv(y, divS);
         const uint32_t b = y - sr * s;
         Count<P> cnt;
-        cnt.add(Lp[(uint64_t)y * W + w]);
+        cnt.add(Lp[(uint64_t)yl * W + w]);
         const uint64_t base = (uint64_t)sr * s;
         for (uint32_t a = 0; a < s; ++a) {
             if (a == b) continue;
-            const uint64_t cs = (base + a) * (s - 1) + (b - (b > a));
+            const uint64_t cs = (base + a) * (s - 1) + (b - (b > a)) - cbase;
             cnt.add(C[cs * W + w]);
         }
-        Rp[(uint64_t)y * W + w] = cnt.ge(thr);
+        Rp[(uint64_t)yl * W + w] = cnt.ge(thr);
     }
 }
 
@@ -126,7 +133,7 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(uint32_t n, uint32_t me, ui
                                                      const uint64_t* __restrict__ scratch,
                                                      uint64_t offF, uint64_t offOB, uint64_t offOO,
                                                      uint64_t offVAL, uint64_t offL0,
-                                                     uint64_t offC1,
+                                                     const uint64_t* __restrict__ C1,
                                                      uint64_t* __restrict__ decisions,
                                                      uint8_t* __restrict__ outcome,
                                                      uint64_t* __restrict__ partial) {
@@ -147,7 +154,7 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(uint32_t n, uint32_t me, ui
                 for (uint32_t a = 0; a < L; ++a) {
                     if (a == b) continue;
                     const uint64_t cs = (uint64_t)a * (L - 1) + (b - (b > a));
-                    cnt.add(scratch[offC1 + cs * W + w]);
+                    cnt.add(C1[cs * W + w]);
                 }
             }
             const uint32_t c = me >= 1 ? L : 1u;  // OM(0): the direct value alone
@@ -288,24 +295,25 @@ hipError_t launch_table(const RunArgs& a, uint64_t* partials) {
 }
 
 template <int P>
-static void launch_majority_p(uint32_t s, uint32_t W, uint32_t work, const uint64_t* Lp,
-                              const uint64_t* C, uint64_t* Rp, hipStream_t st) {
+static void launch_majority_p(uint32_t s, uint32_t W, uint32_t work, uint32_t ybase,
+                              uint32_t cbase, const uint64_t* Lp, const uint64_t* C, uint64_t* Rp,
+                              hipStream_t st) {
     hipLaunchKernelGGL(k_majority<P>, dim3(blocks_for(work, 16384)), dim3(kBlock), 0, st, s,
-                       make_fastdiv(W), make_fastdiv(s), work, Lp, C, Rp);
+                       make_fastdiv(W), make_fastdiv(s), work, ybase, cbase, Lp, C, Rp);
 }
 
 template <int P>
 static void launch_epilogue_p(uint32_t blocks, const RunArgs& a, uint64_t W, uint64_t nt,
-                              const uint64_t* scratch, const LevelsLayout& lay, uint64_t offC1,
+                              const uint64_t* scratch, const LevelsLayout& lay, const uint64_t* C1,
                               uint64_t* dec, uint8_t* out, uint64_t* partials) {
     hipLaunchKernelGGL(k_epilogue<P>, dim3(blocks), dim3(kBlock), 0, a.stream, a.n, a.me, W, nt,
-                       scratch, lay.F, lay.OB, lay.OO, lay.VAL, lay.Lk[0], offC1, dec, out,
+                       scratch, lay.F, lay.OB, lay.OO, lay.VAL, lay.Lk[0], C1, dec, out,
                        partials);
 }
 
 hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_t* d_sender,
                                uint64_t* scratch, const LevelsLayout& lay, uint64_t trial0,
-                               uint64_t ntrials, uint64_t* partials) {
+                               uint64_t ntrials, uint64_t* partials, const LevelsJob& job) {
     const uint64_t W = (ntrials + 63) / 64;
     const uint64_t gw0 = (a.first_trial + trial0) / 64;
     hipStream_t st = a.stream;
@@ -316,54 +324,76 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
                        scratch, W, lay.F, lay.OB, lay.OO, lay.VAL); }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    // where level k / majority p live: scratch, except the level-1 child
+    // results (R_1, or L_1 at depth 1) that a subtree pass leaves in votes_out
+    auto Lptr = [&](uint32_t k) -> uint64_t* {
+        if (k == 1 && g.me == 1 && job.votes_out) return job.votes_out;
+        return scratch + lay.Lk[k];
+    };
+    auto Rptr = [&](uint32_t p) -> uint64_t* {
+        if (p == 1 && job.votes_out) return job.votes_out;
+        return scratch + lay.Rp[p];
+    };
     // relay, top-down (levels 0..me, or 0..me-1 when the leaf level is fused
-    // into the leaf-parent majority and never materialised)
-    const uint32_t ktop = lay.leaf_fused ? g.me - 1 : g.me;
+    // into the leaf-parent majority and never materialised).  Level 0 is
+    // always whole; a root-only pass stops there.
+    const uint32_t ktop = !job.tree ? 0 : (lay.leaf_fused ? g.me - 1 : g.me);
     for (uint32_t k = 0; k <= ktop; ++k) {
-        const uint32_t S = (uint32_t)g.S[k];
-        const uint32_t work = (uint32_t)(((uint64_t)S + 1) / 2 * W);
-        const uint64_t* Lprev = k == 0 ? scratch + lay.OB : scratch + lay.Lk[k - 1];
+        const uint32_t xbase = (uint32_t)lay.base[k], xcnt = (uint32_t)lay.cnt[k];
+        if (xcnt == 0) continue;
+        const uint32_t npair = (xbase + xcnt + 1) / 2 - xbase / 2;
+        const uint32_t work = (uint32_t)((uint64_t)npair * W);
+        const uint64_t* Lprev = k == 0 ? scratch + lay.OB : Lptr(k - 1);
+        const uint32_t pbase = k == 0 ? 0u : (uint32_t)lay.base[k - 1];
         const uint8_t* snd = k == 0 ? nullptr : d_sender + g.sender_off[k - 1];
         ProfScope ps(a.prof, k == g.me ? "k_relay_leaf" : "k_relay_inner", st);
-        hipLaunchKernelGGL(k_relay, dim3(blocks_for(work, 16384)), dim3(kBlock), 0, st, k, S,
-                           g.L - k, make_fastdiv((uint32_t)W), make_fastdiv(g.L - k), work, a.seed,
-                           gw0, Lprev, scratch + lay.Lk[k], scratch + lay.F, snd);
+        hipLaunchKernelGGL(k_relay, dim3(blocks_for(work, 16384)), dim3(kBlock), 0, st, k, xbase,
+                           xcnt, pbase, make_fastdiv((uint32_t)W), make_fastdiv(g.L - k), work,
+                           a.seed, gw0, Lprev, Lptr(k), scratch + lay.F, snd);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    if (lay.leaf_fused) {  // L_me generated on the fly: R_{me-1} straight from L_{me-1}
-        e = launch_leaf(g, a.seed, gw0, (uint32_t)W, scratch + lay.Lk[g.me - 1], scratch + lay.F,
-                        a.members, scratch + lay.Rp[g.me - 1], st, a.prof);
+    if (job.tree && lay.leaf_fused) {  // L_me generated on the fly: R_{me-1} straight from L_{me-1}
+        // leaf blocks = slots of level me-2; level 0 is stored whole, but its
+        // subtree range is the first-hop lieutenants [jb, je) themselves
+        const bool top = g.me == 2;
+        const uint32_t srbase = top ? lay.jb : (uint32_t)lay.base[g.me - 2];
+        const uint32_t srcnt = top ? lay.je - lay.jb : (uint32_t)lay.cnt[g.me - 2];
+        e = launch_leaf(g, a.seed, gw0, (uint32_t)W, srbase, srcnt, Lptr(g.me - 1),
+                        scratch + lay.F, a.members, Rptr(g.me - 1), st, a.prof);
         if (e != hipSuccess) return e;
     }
     // inner majorities, bottom-up (levels me-1..1, or me-2..1 after k_leaf)
-    for (int p = (int)g.me - (lay.leaf_fused ? 2 : 1); p >= 1; --p) {
+    for (int p = job.tree ? (int)g.me - (lay.leaf_fused ? 2 : 1) : 0; p >= 1; --p) {
         const uint32_t s = g.L - (uint32_t)p;
-        const uint32_t work = (uint32_t)(g.S[p] * W);
-        const uint64_t* C = (p + 1 == (int)g.me) ? scratch + lay.Lk[p + 1] : scratch + lay.Rp[p + 1];
-        const uint64_t* Lp = scratch + lay.Lk[p];
-        uint64_t* Rp = scratch + lay.Rp[p];
+        const uint32_t work = (uint32_t)(lay.cnt[p] * W);
+        const uint32_t ybase = (uint32_t)lay.base[p], cbase = (uint32_t)lay.base[p + 1];
+        const uint64_t* C = (p + 1 == (int)g.me) ? Lptr(p + 1) : Rptr(p + 1);
+        const uint64_t* Lp = Lptr(p);
+        uint64_t* Rp = Rptr(p);
         ProfScope ps(a.prof, p + 1 == (int)g.me ? "k_majority_leaf" : "k_majority_inner", st);
         switch (planes_for(s)) {
-            case 1: launch_majority_p<1>(s, (uint32_t)W, work, Lp, C, Rp, st); break;
-            case 2: launch_majority_p<2>(s, (uint32_t)W, work, Lp, C, Rp, st); break;
-            case 3: launch_majority_p<3>(s, (uint32_t)W, work, Lp, C, Rp, st); break;
-            case 4: launch_majority_p<4>(s, (uint32_t)W, work, Lp, C, Rp, st); break;
-            default: launch_majority_p<5>(s, (uint32_t)W, work, Lp, C, Rp, st); break;
+            case 1: launch_majority_p<1>(s, (uint32_t)W, work, ybase, cbase, Lp, C, Rp, st); break;
+            case 2: launch_majority_p<2>(s, (uint32_t)W, work, ybase, cbase, Lp, C, Rp, st); break;
+            case 3: launch_majority_p<3>(s, (uint32_t)W, work, ybase, cbase, Lp, C, Rp, st); break;
+            case 4: launch_majority_p<4>(s, (uint32_t)W, work, ybase, cbase, Lp, C, Rp, st); break;
+            default: launch_majority_p<5>(s, (uint32_t)W, work, ybase, cbase, Lp, C, Rp, st); break;
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    // root + quorum epilogue
-    const uint64_t offC1 = g.me >= 2 ? lay.Rp[1] : (g.me == 1 ? lay.Lk[1] : 0);
+    if (!job.root) return hipSuccess;
+    // root + quorum epilogue over L_0 and the level-1 child results
+    const uint64_t* C1 = job.votes_in ? job.votes_in
+                         : (g.me >= 2 ? scratch + lay.Rp[1] : (g.me == 1 ? scratch + lay.Lk[1] : nullptr));
     const uint32_t blocks = blocks_for(W * 64, kPartialRows);
     uint64_t* dec = a.decisions ? a.decisions + trial0 : nullptr;
     uint8_t* out = a.outcome ? a.outcome + trial0 : nullptr;
     { ProfScope ps(a.prof, "k_epilogue", st);
     switch (planes_for(g.L)) {
-        case 1: launch_epilogue_p<1>(blocks, a, W, ntrials, scratch, lay, offC1, dec, out, partials); break;
-        case 2: launch_epilogue_p<2>(blocks, a, W, ntrials, scratch, lay, offC1, dec, out, partials); break;
-        case 3: launch_epilogue_p<3>(blocks, a, W, ntrials, scratch, lay, offC1, dec, out, partials); break;
-        case 4: launch_epilogue_p<4>(blocks, a, W, ntrials, scratch, lay, offC1, dec, out, partials); break;
-        default: launch_epilogue_p<5>(blocks, a, W, ntrials, scratch, lay, offC1, dec, out, partials); break;
+        case 1: launch_epilogue_p<1>(blocks, a, W, ntrials, scratch, lay, C1, dec, out, partials); break;
+        case 2: launch_epilogue_p<2>(blocks, a, W, ntrials, scratch, lay, C1, dec, out, partials); break;
+        case 3: launch_epilogue_p<3>(blocks, a, W, ntrials, scratch, lay, C1, dec, out, partials); break;
+        case 4: launch_epilogue_p<4>(blocks, a, W, ntrials, scratch, lay, C1, dec, out, partials); break;
+        default: launch_epilogue_p<5>(blocks, a, W, ntrials, scratch, lay, C1, dec, out, partials); break;
     } }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return launch_reduce(partials, (int)blocks, a.counters, st, a.prof);

@@ -159,6 +159,29 @@ int ba_run_trials_device(struct ba_ctx* ctx, const ba_params* p, uint64_t batch,
                          uint64_t* d_decisions, uint8_t* d_outcome, uint64_t* d_counters,
                          void* stream);
 
+/* ---- one huge instance split by first-hop subtree --------
+ * The subtree of first-hop lieutenant j (relay paths starting 0 -> j) needs
+ * only L_0[j]; its relay levels and inner majorities are independent of the
+ * other subtrees.  A rank owning subtrees [j_begin, j_end) (0-based lieutenant
+ * ranks, j_end <= n-1) computes their level-1 child results -- R_1[j.r]
+ * (m_eff >= 2) or L_1[j.r] (m_eff == 1), the votes each lieutenant r counts
+ * about j (ba.py:169-186 generalised) -- into
+ *     d_votes[(j - j_begin)(n-2) + c][w],  w < ceil(batch/64), c < n-2,
+ * 64 trials per uint64 word.  Concatenating every rank's d_votes in j order
+ * (an all-gather) gives the full [(n-1)(n-2)][W] array that
+ * ba_root_from_votes_device turns into the root majorities, quorum and
+ * counters -- bit-identical to ba_run_trials_device on the same params.
+ * LEVELS engine, Philox lies; the batch must fit one scratch chunk
+ * (BA_ETOOBIG otherwise: split the batch). */
+uint64_t ba_vote_slots(uint32_t n, uint32_t m, uint32_t j_begin, uint32_t j_end);
+int ba_subtree_votes_device(struct ba_ctx* ctx, const ba_params* p, uint64_t batch,
+                            uint32_t j_begin, uint32_t j_end, const uint32_t* d_faulty_mask,
+                            const uint8_t* d_order, uint64_t* d_votes, void* stream);
+int ba_root_from_votes_device(struct ba_ctx* ctx, const ba_params* p, uint64_t batch,
+                              const uint32_t* d_faulty_mask, const uint8_t* d_order,
+                              const uint64_t* d_votes, uint64_t* d_decisions, uint8_t* d_outcome,
+                              uint64_t* d_counters, void* stream);
+
 /* Per-kernel timing (tracing aux subsystem; replaces nothing in ba.py, which
  * only prints).  When enabled, every kernel the ctx launches is bracketed by
  * HIP events on its launch stream; ba_profile_read syncs those events and

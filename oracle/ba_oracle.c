@@ -321,3 +321,45 @@ int ba_oracle_run(uint32_t n, uint32_t m, uint64_t seed, uint32_t lie_mode,
     if (counters) memcpy(counters, total, sizeof total);
     return 0;
 }
+
+/* Level-1 child results of the first-hop split (include/ba.h ba_subtree_votes_device):
+ * votes[(i * L + j) * (L - 1) + c] = resolve_r(j) for trial i, first-hop
+ * lieutenant rank j, and receiver rank r = c + (c >= j): R_1[j.r] (me >= 2) or
+ * L_1[j.r] (me == 1) -- what r concludes about j's relay (ba.py:169-186
+ * generalised).  Returns 0 or a negative error code (E_NOTSUP for me == 0). */
+int ba_oracle_votes(uint32_t n, uint32_t m, uint64_t seed, uint32_t faulty_mode, uint32_t f,
+                    uint32_t order_mode, uint32_t order_value, uint64_t first_trial,
+                    uint64_t batch, const uint32_t* faulty, const uint8_t* order, uint8_t* votes,
+                    int threads) {
+    if (n < 3 || n > MAXN || m > MAXM) return E_INVAL;
+    if (faulty_mode == FAULTY_GIVEN && !faulty) return E_INVAL;
+    if (order_mode == ORDER_GIVEN && !order) return E_INVAL;
+    if (first_trial & 63) return E_INVAL;
+    const int L = (int)n - 1;
+    const int me = (int)m < (int)n - 2 ? (int)m : (int)n - 2;
+    if (me < 1) return E_NOTSUP;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#else
+    (void)threads;
+#endif
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t i = 0; i < (int64_t)batch; ++i) {
+        uint64_t t = first_trial + (uint64_t)i;
+        uint32_t fmask = faulty_mode == FAULTY_GIVEN ? faulty[i] : 0;
+        uint8_t oc = order_mode == ORDER_GIVEN ? order[i] : 0;
+        ba_oracle_gen(n, seed, faulty_mode, f, order_mode, order_value, t,
+                      faulty_mode == FAULTY_GIVEN ? NULL : &fmask,
+                      order_mode == ORDER_GIVEN ? NULL : &oc);
+        fmask &= (n >= 32) ? 0xFFFFFFFFu : ((1u << n) - 1u);
+        tctx c = {seed, t, L, me, fmask, oc == V_ATTACK};
+        int path[MAXM + 2];
+        for (int j = 0; j < L; ++j)
+            for (int k = 0; k < L - 1; ++k) {
+                int r = k + (k >= j);
+                path[0] = j;
+                votes[((uint64_t)i * L + j) * (L - 1) + k] = (uint8_t)om_resolve(&c, path, 1, r, 1u << j);
+            }
+    }
+    return 0;
+}

@@ -45,6 +45,13 @@ int ba_oracle_run(uint32_t n, uint32_t m, uint64_t seed, uint32_t lie_mode,
                   const uint32_t* table, const uint32_t* poll, uint64_t* decisions,
                   uint8_t* outcome, uint64_t* counters, int threads);
 
+/* Level-1 child results per (trial, first-hop j, receiver) for the first-hop
+ * split (see ba_oracle.c).  votes: batch * (n-1) * (n-2) bytes, 0/1. */
+int ba_oracle_votes(uint32_t n, uint32_t m, uint64_t seed, uint32_t faulty_mode, uint32_t f,
+                    uint32_t order_mode, uint32_t order_value, uint64_t first_trial,
+                    uint64_t batch, const uint32_t* faulty, const uint8_t* order, uint8_t* votes,
+                    int threads);
+
 #ifdef __cplusplus
 }
 #endif

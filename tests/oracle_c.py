@@ -30,6 +30,8 @@ def load():
         lib.ba_oracle_lie.restype = u32
         lib.ba_oracle_philox.argtypes = [vp, vp, vp]
         lib.ba_oracle_gen.argtypes = [u32, u64, u32, u32, u32, u32, u64, vp, vp]
+        lib.ba_oracle_votes.argtypes = [u32, u32, u64, u32, u32, u32, u32, u64, u64, vp, vp, vp,
+                                        ctypes.c_int]
         _lib = lib
     return _lib
 
@@ -58,3 +60,30 @@ def run(n, m, batch, seed=0, lie_mode=0, faulty_mode=0, f=0, order_mode=0, order
     if rc != 0:
         raise RuntimeError(f"oracle rc={rc}")
     return dec, out, dict(zip(COUNTER_NAMES, [int(x) for x in cnt[:12]]))
+
+
+def votes(n, m, batch, seed=0, faulty_mode=0, f=0, order_mode=0, order_value=1, first_trial=0,
+          faulty=None, order=None, threads=0):
+    """Level-1 child results uint8[batch, n-1, n-2] (see ba_oracle_votes)."""
+    lib = load()
+    faulty = None if faulty is None else np.ascontiguousarray(faulty, np.uint32)
+    order = None if order is None else np.ascontiguousarray(order, np.uint8)
+    out = np.zeros((batch, n - 1, n - 2), np.uint8)
+    rc = lib.ba_oracle_votes(n, m, seed, faulty_mode, f, order_mode, order_value, first_trial,
+                             batch, _p(faulty), _p(order), _p(out), threads)
+    if rc != 0:
+        raise RuntimeError(f"oracle rc={rc}")
+    return out
+
+
+def pack_votes(v, jb=0, je=None):
+    """uint8[batch, L, L-1] -> the library's vote layout uint64[(je-jb)(L-1), W]."""
+    batch, L, _ = v.shape
+    je = L if je is None else je
+    W = (batch + 63) // 64
+    flat = v[:, jb:je, :].reshape(batch, -1)
+    pad = np.zeros((W * 64, flat.shape[1]), np.uint8)
+    pad[:batch] = flat
+    bits = pad.reshape(W, 64, -1).transpose(2, 0, 1)  # slot, word, lane
+    weights = (np.uint64(1) << np.arange(64, dtype=np.uint64))
+    return (bits.astype(np.uint64) * weights).sum(axis=2, dtype=np.uint64)
