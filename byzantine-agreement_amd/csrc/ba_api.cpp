@@ -165,7 +165,11 @@ struct DevBuf {
     size_t bytes = 0;
     int grow(size_t need) {
         if (need <= bytes) return BA_OK;
-        if (p) (void)hipFree(p);
+        // kernels queued on any stream may still use the old buffer
+        if (p) {
+            (void)hipDeviceSynchronize();
+            (void)hipFree(p);
+        }
         p = nullptr;
         bytes = 0;
         if (need == 0) return BA_OK;
@@ -445,7 +449,7 @@ static RunArgs make_args(ba_ctx* ctx, const ba_params* p, uint64_t batch, const 
     a.decisions = d_decisions;
     a.outcome = d_outcome;
     a.counters = d_counters;
-    a.stream = stream ? (hipStream_t)stream : ctx->stream;
+    a.stream = (hipStream_t)stream;  // NULL = HIP's null stream (HIP convention)
     a.prof = &ctx->prof;
     a.cu_count = ctx->cu_count;
     return a;

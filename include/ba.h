@@ -150,8 +150,9 @@ int ba_run_trials(struct ba_ctx* ctx, const ba_params* p, uint64_t batch,
                   const uint32_t* lie_table, const uint32_t* poll_commander,
                   uint64_t* decisions, uint8_t* outcome, ba_counters* counters);
 
-/* Same computation on device buffers, enqueued on `stream` (hipStream_t, NULL =
- * the ctx stream).  d_counters (BA_NCOUNTERS uint64 on device) is ACCUMULATED
+/* Same computation on device buffers, enqueued on `stream` (a hipStream_t as
+ * void*; NULL is HIP's null stream, as in every HIP API -- NOT the ctx stream,
+ * which only the host-pointer entry point uses).  d_counters (BA_NCOUNTERS uint64 on device) is ACCUMULATED
  * into, so repeated calls sum; zero it first for one call's totals. */
 int ba_run_trials_device(struct ba_ctx* ctx, const ba_params* p, uint64_t batch,
                          const uint32_t* d_faulty_mask, const uint8_t* d_order,
@@ -171,6 +172,7 @@ int ba_run_trials_device(struct ba_ctx* ctx, const ba_params* p, uint64_t batch,
  * (an all-gather) gives the full [(n-1)(n-2)][W] array that
  * ba_root_from_votes_device turns into the root majorities, quorum and
  * counters -- bit-identical to ba_run_trials_device on the same params.
+ * Both are asynchronous on `stream` (NULL = HIP's null stream).
  * LEVELS engine, Philox lies; the batch must fit one scratch chunk
  * (BA_ETOOBIG otherwise: split the batch). */
 uint64_t ba_vote_slots(uint32_t n, uint32_t m, uint32_t j_begin, uint32_t j_end);
