@@ -66,6 +66,25 @@ def kernel_bytes(name: str, n: int, m: int, batch: int) -> int:
     return 0
 
 
+def pmc_traffic(n: int, m: int, batch: int, engine: str, kernel: str):
+    """HBM traffic per launch of `kernel` from the newest committed rocprofv3 PMC
+    summary of this exact workload (profiles/*pmc*.json, tools/pmc_summary.py;
+    FETCH_SIZE doubled per MI355X_MICROARCH.md), or (None, None, None)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        c = d.get("config") or {}
+        if (c.get("n"), c.get("m"), c.get("batch"), c.get("engine")) != (n, m, batch, engine):
+            continue
+        for name, e in d.get("kernels", {}).items():
+            if kernel in name and "traffic_bytes" in e:
+                return e["traffic_bytes"], e.get("valu_util"), os.path.relpath(path, ROOT)
+    return None, None, None
+
+
 def run_cpu_baseline(n, m, seed, fmax, budget_s):
     """Time the C oracle (oracle/ba_oracle.c, OpenMP) on a bounded sample of the
     same synthetic workload (same seed, first trials of the stream)."""
@@ -180,10 +199,14 @@ def main():
             avg_ms = ms / nl
             alg = kernel_bytes(name, n, m, B)
             achieved = alg / (avg_ms * 1e-3) / 1e9 if alg else None
+            traffic, valu, src = pmc_traffic(n, m, B, args.engine, name)
             roof = {"bound": "hbm", "kernel": name, "avg_ms": round(avg_ms, 4),
                     "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                    "traffic": None, "algorithmic_bytes_per_launch": alg}
+                    "traffic": round(traffic) if traffic else None,
+                    "algorithmic_bytes_per_launch": alg,
+                    "traffic_source": src,
+                    "valu_util": round(valu, 4) if valu else None}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = run_cpu_baseline(n, m, args.seed, fmax, args.cpu_budget_s)

@@ -134,7 +134,7 @@ __global__ __launch_bounds__(kFusedThreads, (S <= 7 ? 4 : 2)) void k_fused(
     uint64_t batch, const uint32_t* __restrict__ faulty, const uint8_t* __restrict__ order,
     const uint8_t* __restrict__ sender, const uint64_t* __restrict__ members,
     uint64_t* __restrict__ decisions,
-    uint8_t* __restrict__ outcome, uint64_t* __restrict__ partial) {
+    uint8_t* __restrict__ outcome, uint64_t* __restrict__ counters) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     // run counters live in LDS (not in registers across the leaf stage)
     __shared__ __attribute__((aligned(16))) unsigned long long blockcnt[16];
@@ -319,7 +319,9 @@ __global__ __launch_bounds__(kFusedThreads, (S <= 7 ? 4 : 2)) void k_fused(
         __syncthreads();
         FUSED_STAMP(5);
     }
-    if (tid < 16) partial[(uint64_t)blockIdx.x * 16 + tid] = blockcnt[tid];
+    // integer sums commute: one device-scope atomic per counter per block keeps
+    // the totals deterministic and saves the separate k_reduce launch
+    if (tid < C_NUM && blockcnt[tid]) atomicAdd((unsigned long long*)&counters[tid], blockcnt[tid]);
     FUSED_STAMP_STORE();
 }
 
@@ -349,7 +351,7 @@ __global__ __launch_bounds__(kFusedThreads, ((N - 3) <= 7 ? 4 : 2)) void k_fused
     uint32_t wpb, uint64_t seed, GenSpec gs, uint64_t first_trial, uint64_t batch,
     const uint32_t* __restrict__ faulty, const uint8_t* __restrict__ order,
     uint64_t* __restrict__ decisions, uint8_t* __restrict__ outcome,
-    uint64_t* __restrict__ partial) {
+    uint64_t* __restrict__ counters) {
     using G = Om3<N>;
     constexpr int L = G::L, S = G::S, S1 = G::S1, STRIDE = G::words;
     constexpr uint32_t ME = 3;
@@ -515,7 +517,9 @@ __global__ __launch_bounds__(kFusedThreads, ((N - 3) <= 7 ? 4 : 2)) void k_fused
         __syncthreads();
         FUSED_STAMP(5);
     }
-    if (tid < 16) partial[(uint64_t)blockIdx.x * 16 + tid] = blockcnt[tid];
+    // integer sums commute: one device-scope atomic per counter per block keeps
+    // the totals deterministic and saves the separate k_reduce launch
+    if (tid < C_NUM && blockcnt[tid]) atomicAdd((unsigned long long*)&counters[tid], blockcnt[tid]);
     FUSED_STAMP_STORE();
 }
 
@@ -610,7 +614,7 @@ static void launch_fused_s(const FusedPlan& fp, const FusedPlan* d_fp, uint32_t 
                            uint64_t* partials) {
     hipLaunchKernelGGL(k_fused<S>, dim3(blocks), dim3(fp.threads), lds_bytes, a.stream, d_fp,
                        a.seed, a.gen, a.first_trial, a.batch, a.faulty, a.order, d_sender, a.members,
-                       a.decisions, a.outcome, partials);
+                       a.decisions, a.outcome, a.counters);
 }
 
 hipError_t launch_fused(const RunArgs& a, const Geometry& g, const FusedPlan& fp,
@@ -664,7 +668,7 @@ hipError_t launch_fused(const RunArgs& a, const Geometry& g, const FusedPlan& fp
     case nn:                                                                                     \
         hipLaunchKernelGGL(k_fused3<nn>, dim3(blocks), dim3(kFusedThreads), lds_bytes, a.stream, \
                            fp.wpb, a.seed, a.gen, a.first_trial, a.batch, a.faulty, a.order,     \
-                           a.decisions, a.outcome, partials);                                   \
+                           a.decisions, a.outcome, a.counters);                                 \
         break;
                 FUSED3_CASE(5) FUSED3_CASE(6) FUSED3_CASE(7) FUSED3_CASE(8) FUSED3_CASE(9)
                 FUSED3_CASE(10) FUSED3_CASE(11) FUSED3_CASE(12) FUSED3_CASE(13) FUSED3_CASE(14)
@@ -684,7 +688,8 @@ hipError_t launch_fused(const RunArgs& a, const Geometry& g, const FusedPlan& fp
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    return launch_reduce(partials, (int)blocks, a.counters, a.stream, a.prof);
+    (void)partials;
+    return hipSuccess;
 }
 
 }  // namespace ba

@@ -2,7 +2,7 @@
 # GPU-box session: every GPU step has its own time limit; a fault, abort or
 # timeout ends the session (no retries).  Logs land in gpurun_out/.
 # usage: tools/gpu_session.sh [stage ...]
-#   tests smoke bench bench_levels bench_fused prof pmc philox
+#   tests smoke bench bench_levels bench_fused prof pmc philox configs
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -40,7 +40,10 @@ for s in $STAGES; do
     pmc) pmc_pass sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY || exit $?
          pmc_pass fetch FETCH_SIZE GRBM_GUI_ACTIVE GRBM_COUNT || exit $?
          pmc_pass write WRITE_SIZE || exit $?
-         pmc_pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR || exit $? ;;
+         pmc_pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR || exit $?
+         python3 tools/pmc_summary.py gpurun_out/pmc gpurun_out/pmc_summary.json \
+           --workload "bench.py default: n=10 m=3, 1048576 trials/step" --config 10,3,1048576,auto,k_fused > gpurun_out/pmc_summary.log 2>&1 ;;
+    configs) run configs 600 python -u tools/run_configs.py || exit $? ;;
     *) echo "unknown stage $s"; exit 2 ;;
   esac
 done

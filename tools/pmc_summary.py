@@ -1,6 +1,7 @@
 """Summarise rocprofv3 --pmc passes (tools/gpu_session.sh `pmc` stage) per kernel.
 
 usage: python tools/pmc_summary.py <pmc dir> <out.json> [--workload TEXT]
+                                  [--config n,m,batch,engine,kernel]
 
 Per kernel: the mean per dispatch of every counter, plus the derived figures
 DESIGN.md §Measurement uses:
@@ -27,6 +28,10 @@ SIMDS = 256 * 4
 def main():
     d, out = sys.argv[1], sys.argv[2]
     workload = sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else ""
+    config = None
+    if "--config" in sys.argv:
+        n, m, batch, engine, kernel = sys.argv[sys.argv.index("--config") + 1].split(",")
+        config = {"n": int(n), "m": int(m), "batch": int(batch), "engine": engine, "kernel": kernel}
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in sorted(glob.glob(os.path.join(d, "*counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
@@ -44,7 +49,8 @@ def main():
             e["kernel_cycles"] = cyc
             e["valu_util"] = mean["SQ_INSTS_VALU"] * 2 / (SIMDS * cyc)
         res[k] = e
-    json.dump({"source": d, "workload": workload, "kernels": res}, open(out, "w"), indent=1)
+    json.dump({"source": d, "workload": workload, "config": config, "kernels": res},
+              open(out, "w"), indent=1)
     for k, e in res.items():
         print(k[:50], {x: e[x] for x in e if x not in ("counters",)})
 

@@ -1,0 +1,123 @@
+"""BASELINE.json configs 3-5 (the non-headline ones) through ba_amd.dist.
+
+    python tools/run_configs.py [--only 3,4,5]                       # one GPU
+    python -m torch.distributed.run --nproc-per-node N tools/run_configs.py  # N GPUs
+
+  3  n=13, m=4, 64M trials, trial-DP across ranks (counters all-reduced)
+  4  n=10, m=3 faulty-count sweep f = 0..n/3+1, exactly f faulty, 1M trials each:
+     agreement (IC1) / validity (IC2) / quorum-outcome breakdown curve
+  5  n=16, m=5: one instance split by first-hop subtree (latency), and a batch
+     of 1024 instances (throughput), votes all-gathered across ranks
+
+Rank 0 prints one JSON line per config.  Timings bracket the device work with
+torch.cuda.synchronize() (+ a barrier across ranks) and take the max over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "byzantine-agreement_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from ba_amd import dist as D  # noqa: E402
+from ba_amd import lib as L  # noqa: E402
+
+
+def timed(fn, world, dev):
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    out = fn()
+    torch.cuda.synchronize(dev)
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    return out, float(dt.item())
+
+
+def counters(t):
+    return dict(zip(L.COUNTER_NAMES, [int(x) for x in t.cpu().tolist()]))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="3,4,5")
+    ap.add_argument("--trials3", type=int, default=64 << 20)
+    ap.add_argument("--trials4", type=int, default=1 << 20)
+    ap.add_argument("--batch5", type=int, default=1024)
+    a = ap.parse_args()
+    which = {int(x) for x in a.only.split(",")}
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    eng = L.Engine(local)
+    be = D.DeviceBackend(eng, dev)
+    out = []
+
+    if 3 in which:
+        n, m, T = 13, 4, a.trials3
+        D.run_trials_dp(be, n, m, 1 << 16, f=4)  # warm-up: geometry, scratch
+        cnt, dt = timed(lambda: D.run_trials_dp(be, n, m, T, f=4), world, dev)
+        out.append({"config": 3, "workload": f"OM({m}) n={n}, {T} trials, f~U{{0..4}}, "
+                    f"trial-DP over {world} GPU(s), counters all-reduced",
+                    "trials_per_s": T / dt, "seconds": dt, "n_gpus": world,
+                    "counters": counters(cnt)})
+
+    if 4 in which:
+        n, m, T = 10, 3, a.trials4
+        D.run_trials_dp(be, n, m, 1 << 16, f=1)  # warm-up
+        rows = []
+        for f in range(0, (n - 1) // 3 + 2):
+            cnt, dt = timed(lambda: D.run_trials_dp(be, n, m, T, f=f, faulty_mode=L.FAULTY_EXACT,
+                                                    base_trial=T * f), world, dev)
+            c = counters(cnt)
+            rows.append({"f": f, "agreement": c["agreement"] / T,
+                         "validity": c["validity"] / max(1, c["validity_applicable"]),
+                         "quorum_attack": c["quorum_attack"] / T,
+                         "quorum_retreat": c["quorum_retreat"] / T,
+                         "quorum_undetermined": c["quorum_undetermined"] / T,
+                         "undefined_decisions_per_trial": c["undefined_decisions"] / T,
+                         "bound_violations": c["bound_violations"], "trials_per_s": T / dt})
+        out.append({"config": 4, "workload": f"OM({m}) n={n}, exactly f faulty, {T} trials "
+                    "per point", "n_gpus": world, "sweep": rows})
+
+    if 5 in which:
+        n, m = 16, 5
+        res = {}
+        for B in (1, a.batch5):
+            p = L.make_params(n, m, 0xBA5EED, L.LIE_PHILOX, L.FAULTY_RANDOM, 5, L.ORDER_RANDOM,
+                              L.ATTACK, L.ENGINE_LEVELS, 0)
+            D.run_instance_split(be, p, B)  # warm-up
+            reps = 10 if B == 1 else 3
+            (dec, o, cnt), dt = timed(lambda: [D.run_instance_split(be, p, B)
+                                               for _ in range(reps)][-1], world, dev)
+            res[B] = {"seconds_per_call": dt / reps, "instances_per_s": B * reps / dt,
+                      "counters": counters(cnt)}
+        out.append({"config": 5, "workload": f"OM({m}) n={n} (3,999,675 tree slots), first-hop "
+                    f"subtree split over {world} GPU(s), votes all-gathered",
+                    "latency_one_instance_ms": res[1]["seconds_per_call"] * 1e3,
+                    "batch": a.batch5, "throughput_instances_per_s": res[a.batch5]["instances_per_s"],
+                    "n_gpus": world, "counters_batch": res[a.batch5]["counters"]})
+
+    if rank == 0:
+        for line in out:
+            print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
