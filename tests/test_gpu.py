@@ -251,3 +251,27 @@ def test_engines_agree_with_and_without_leaf_fusion(monkeypatch, n, m):
 def test_fused_engine_selected_for_bench_config():
     from ba_amd import lib as L
     assert L.load().ba_engine_for(10, 3) == L.ENGINE_FUSED
+
+
+@pytest.mark.parametrize("n", [4, 10, 16])
+def test_philox_om1_equals_table_mode_gpu(engine, n):
+    """On the device: OM(1) with Philox lies (LEVELS kernels) equals the ba.py
+    table-mode kernel fed the same lies in ba.py's canonical draw order."""
+    import ctypes
+    from test_oracle import philox_as_ba_py_table
+    from ba_amd import lib as L
+    B, seed, f = 500, 23, n // 3 + 1
+    res_p = engine.run(n, 1, B, seed=seed, faulty_mode=L.FAULTY_RANDOM, f=f,
+                       order_mode=L.ORDER_RANDOM)
+    lib = oracle_c.load()
+    fms, ocs = [], []
+    for t in range(B):
+        fm, oc = ctypes.c_uint32(), ctypes.c_uint8()
+        lib.ba_oracle_gen(n, seed, 1, f, 1, 1, t, ctypes.byref(fm), ctypes.byref(oc))
+        fms.append(fm.value)
+        ocs.append(oc.value)
+    tab = L.pack_coins([philox_as_ba_py_table(n, seed, t, fms[t]) for t in range(B)], n)
+    res_t = engine.run(n, 1, B, lie_mode=L.LIE_TABLE, faulty=fms, order=ocs, table=tab)
+    same(res_p.decisions, res_t.decisions, "decisions")
+    same(res_p.outcome, res_t.outcome, "outcome")
+    assert res_p.counters == res_t.counters

@@ -195,3 +195,43 @@ def test_header_constants_agree():
     names = re.findall(r"#define BA_C_\w+ (\d+)", hdr)
     assert [int(x) for x in names] == list(range(len(L.COUNTER_NAMES)))
     assert L.COUNTER_NAMES == O.COUNTERS == oracle_c.COUNTER_NAMES
+
+
+def philox_as_ba_py_table(n, seed, t, fm):
+    """The Philox lies of an OM(1) trial, laid out as ba.py's canonical coin
+    sequence: the commander's coins for lieutenants 1..n-1 (ba.py:263-273), then
+    receiver-major: for r = 1..n-1, for j != r faulty, the coin j tells r
+    (ba.py:169-186).  Level-1 slot of (j, r) = j'(L-1) + r' - [r' > j']."""
+    L = n - 1
+    coins = []
+    if fm & 1:
+        coins += [O.lie(seed, t, 0, r) for r in range(L)]
+    for r in range(L):
+        for j in range(L):
+            if j != r and (fm >> (j + 1)) & 1:
+                coins.append(O.lie(seed, t, 1, j * (L - 1) + r - (r > j)))
+    return coins
+
+
+@pytest.mark.parametrize("n", [3, 4, 7, 10, 13])
+def test_om_recursion_at_m1_is_ba_py_rule(n):
+    """Links the OM(m) recursion (Philox lies) to ba.py: at m=1 it equals the
+    table-mode restatement -- pinned on ba.py's own fixtures above -- fed the
+    same lies in ba.py's draw order."""
+    from ba_amd.lib import pack_coins
+    B = 300
+    kw = dict(seed=17, faulty_mode=1, f=n // 2, order_mode=1)
+    dec_p, out_p, cnt_p = oracle_c.run(n, 1, B, **kw)
+    fms, ocs = [], []
+    lib = oracle_c.load()
+    import ctypes
+    for t in range(B):
+        fm, oc = ctypes.c_uint32(), ctypes.c_uint8()
+        lib.ba_oracle_gen(n, 17, 1, n // 2, 1, 1, t, ctypes.byref(fm), ctypes.byref(oc))
+        fms.append(fm.value)
+        ocs.append(oc.value)
+    tab = pack_coins([philox_as_ba_py_table(n, 17, t, fms[t]) for t in range(B)], n)
+    dec_t, out_t, cnt_t = oracle_c.run(n, 1, B, lie_mode=1, faulty=fms, order=ocs, table=tab)
+    assert np.array_equal(dec_p, dec_t)
+    assert np.array_equal(out_p, out_t)
+    assert cnt_p == cnt_t
