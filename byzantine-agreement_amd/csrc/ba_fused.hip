@@ -34,14 +34,16 @@ __device__ __forceinline__ void static_for(F&& f) {
 
 // Column majorities of one leaf block.  diag[a] = L_{me-1}[sigma.j_a] (the
 // direct value, also every loyal row's broadcast), Fm[a] = faulty word of j_a.
+// Column b counts diag[b] then rows a != b in row order, so the carry-save
+// counters see a compile-time input schedule (Csa, ba_device.hpp).
 template <int S>
 __device__ __forceinline__ void leaf_block(uint32_t me, uint64_t seed, uint64_t gw, uint32_t sr,
                                            const uint64_t (&diag)[S], const uint64_t (&Fm)[S],
                                            uint64_t (&R)[S]) {
-    constexpr int P = planes_c(S);
+    constexpr int NL = planes_c(S);
     constexpr int NPAIR = S * (S - 1) / 2;
-    Count<P> cnt[S];
-    static_for<0, S>([&](auto b) { cnt[b()].add(diag[b()]); });
+    Csa<NL> cnt[S];
+    static_for<0, S>([&](auto b) { cnt[b()].template add<0>(diag[b()]); });
     const uint32_t pair0 = sr * (uint32_t)NPAIR;  // leaf block base slot sr*S*(S-1) is even
     static_for<0, NPAIR>([&](auto q) {
         uint64_t lw[2];
@@ -51,10 +53,12 @@ __device__ __forceinline__ void leaf_block(uint32_t me, uint64_t seed, uint64_t 
             constexpr int a = e / (S - 1);
             constexpr int c = e % (S - 1);
             constexpr int b = c + (c >= a);      // receiver's rank among the S members
-            cnt[b].add((Fm[a] & lw[h()]) | (~Fm[a] & diag[a]));
+            constexpr int K = 1 + a - (b < a ? 1 : 0);  // inputs column b holds so far
+            cnt[b].template add<K>((Fm[a] & lw[h()]) | (~Fm[a] & diag[a]));
         });
     });
-    static_for<0, S>([&](auto b) { R[b()] = cnt[b()].ge(S / 2 + 1); });  // inner tie -> non-attack
+    // S inputs per column; strict majority, inner tie -> non-attack
+    static_for<0, S>([&](auto b) { R[b()] = cnt[b()].template ge<S, S / 2 + 1>(); });
 }
 
 // Bit-sliced count of one matrix column in an LDS word image: the direct value

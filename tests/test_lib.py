@@ -64,3 +64,13 @@ def test_no_device_fails_loudly():
     with pytest.raises(L.BAError) as ei:
         L.Engine(0)
     assert ei.value.code == L.EDEVICE
+
+
+def test_carry_save_counter_host_check(tmp_path):
+    """ba_device.hpp's compile-time carry-save counter (used by the leaf blocks)
+    equals popcount >= T for every input count <= 16 (host build, no device)."""
+    exe = tmp_path / "csa_check"
+    src = os.path.join(ROOT, "tests", "native", "csa_check.cpp")
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-o", str(exe), src], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout
