@@ -207,6 +207,7 @@ struct ba_ctx {
     size_t scratch_budget = 8ull << 30;
     bool leaf_fusion = true;  // LEVELS uses k_leaf when available (BA_NO_LEAF_FUSION=1: off)
     DevBuf scratch, partials, io_faulty, io_order, io_table, io_poll, io_dec, io_out, io_cnt;
+    DevBuf sink;  // counter sink replicas + tickets (zeroed once; kernels leave them zero)
     std::map<uint64_t, std::unique_ptr<GeoEntry>> geos;
     Prof prof;
     std::map<std::string, ProfTotal> prof_totals;
@@ -307,6 +308,13 @@ extern "C" int ba_ctx_create(int device, ba_ctx** out) {
         delete ctx;
         return fail(BA_EDEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
     }
+    if (ctx->sink.grow(kSinkBytes) != BA_OK || hipMemset(ctx->sink.p, 0, kSinkBytes) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {
+        (void)hipStreamDestroy(ctx->stream);
+        ctx->sink.release();
+        delete ctx;
+        return fail(BA_ENOMEM, "counter sink allocation failed");
+    }
     *out = ctx;
     return BA_OK;
 }
@@ -317,7 +325,7 @@ extern "C" void ba_ctx_destroy(ba_ctx* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     prof_collect(ctx);
     for (hipEvent_t e : ctx->prof.pool) (void)hipEventDestroy(e);
-    for (DevBuf* b : {&ctx->scratch, &ctx->partials, &ctx->io_faulty, &ctx->io_order, &ctx->io_table,
+    for (DevBuf* b : {&ctx->sink, &ctx->scratch, &ctx->partials, &ctx->io_faulty, &ctx->io_order, &ctx->io_table,
                       &ctx->io_poll, &ctx->io_dec, &ctx->io_out, &ctx->io_cnt})
         b->release();
     for (auto& kv : ctx->geos) {
@@ -452,6 +460,8 @@ static RunArgs make_args(ba_ctx* ctx, const ba_params* p, uint64_t batch, const 
     a.stream = (hipStream_t)stream;  // NULL = HIP's null stream (HIP convention)
     a.prof = &ctx->prof;
     a.cu_count = ctx->cu_count;
+    a.sink.rep = (unsigned long long*)ctx->sink.p;
+    a.sink.ticket = (unsigned int*)((char*)ctx->sink.p + kSinkReplicas * kSinkRepStride * 8);
     return a;
 }
 

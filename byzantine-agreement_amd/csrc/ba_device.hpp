@@ -319,6 +319,50 @@ __device__ __forceinline__ void wave_counts_add(bool live, const TrialResult& r,
     }
 }
 
+// ---------------------------------------------------------------------------
+// Run counter sink.  Device-scope atomics execute at the memory side, one
+// request at a time per cache line, so thousands of waves adding into the
+// caller's 12 counters (one line) at the end of a launch serialise: measured
+// ~130 us for 2048 waves x 12 single-lane adds.  Instead each reporting unit
+// (a wave or a block) adds its totals with ONE 12-lane instruction into
+// replica (unit % R), every replica on lines of its own, then takes a ticket
+// on that replica; the unit whose ticket completes the replica reads it back
+// with atomic exchanges (resetting it for the next launch) and adds it into
+// the caller's counters.  At most R units touch the caller's line.
+// Units of one launch must all call sink_counters exactly once.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSinkReplicas = 64;
+constexpr uint32_t kSinkRepStride = 16;     // uint64 per replica (128 B)
+constexpr uint32_t kSinkTicketStride = 32;  // uint32 per ticket (128 B)
+constexpr size_t kSinkBytes = kSinkReplicas * (kSinkRepStride * 8 + kSinkTicketStride * 4);
+
+struct Sink {
+    unsigned long long* rep;  // [kSinkReplicas][kSinkRepStride], zero between launches
+    unsigned int* ticket;     // [kSinkReplicas][kSinkTicketStride], zero between launches
+};
+
+// Called by every lane of one wave; lane c < C_NUM passes the unit's total of
+// counter c in v (other lanes: ignored).
+__device__ __forceinline__ void sink_counters(uint32_t lane, uint64_t v, uint32_t unit,
+                                              uint32_t nunits, uint64_t* __restrict__ out,
+                                              const Sink& sk) {
+    const uint32_t r = unit % kSinkReplicas;
+    const uint32_t members = (nunits - r + kSinkReplicas - 1) / kSinkReplicas;
+    unsigned long long* rep = sk.rep + r * kSinkRepStride;
+    if (lane < C_NUM && v) atomicAdd(rep + lane, (unsigned long long)v);
+    __builtin_amdgcn_s_waitcnt(0);  // the adds are performed before the ticket
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(sk.ticket + r * kSinkTicketStride, 1u);
+    t = __shfl(t, 0, 64);
+    if (t + 1 == members) {  // last unit of this replica: fold it into `out`
+        if (lane < C_NUM) {
+            const unsigned long long tot = atomicExch(rep + lane, 0ull);
+            if (tot) atomicAdd((unsigned long long*)out + lane, tot);
+        }
+        if (lane == 0) atomicExch(sk.ticket + r * kSinkTicketStride, 0u);
+    }
+}
+
 __device__ __forceinline__ void finish_trial(uint32_t n, uint32_t me, uint32_t fm, uint32_t oc,
                                              uint32_t A, uint32_t U, uint64_t& dec,
                                              uint32_t& out, TrialCounts& tc) {

@@ -42,6 +42,7 @@ struct RunArgs {
     uint64_t* decisions = nullptr;
     uint8_t* outcome = nullptr;
     uint64_t* counters = nullptr;  // BA_NCOUNTERS, accumulated into
+    Sink sink{};                   // ctx-owned counter reduction slots (FUSED / WAVE)
     hipStream_t stream = nullptr;
     Prof* prof = nullptr;
     const uint64_t* members = nullptr;  // device copy of Geometry::members
@@ -105,6 +106,7 @@ constexpr int kMaxLeafS = 12;       // leaf-fused kernels instantiated for S = n
 constexpr int kFusedMaxDepth = 6;
 constexpr uint64_t kFusedLdsBudget = 39 * 1024;  // per block: four blocks per CU
 constexpr int kFusedThreads = 256;               // 4 waves: 4 blocks/CU at <= 128 VGPRs
+constexpr int kWaveThreads = 256;                // WAVE engine: 4 independent waves per block
 
 // LDS image of the FUSED engine (one per 64-trial word, WPB words per block).
 struct FusedPlan {

@@ -138,7 +138,7 @@ __global__ __launch_bounds__(kFusedThreads, (S <= 7 ? 4 : 2)) void k_fused(
     uint64_t batch, const uint32_t* __restrict__ faulty, const uint8_t* __restrict__ order,
     const uint8_t* __restrict__ sender, const uint64_t* __restrict__ members,
     uint64_t* __restrict__ decisions,
-    uint8_t* __restrict__ outcome, uint64_t* __restrict__ counters) {
+    uint8_t* __restrict__ outcome, uint64_t* __restrict__ counters, Sink sk) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     // run counters live in LDS (not in registers across the leaf stage)
     __shared__ __attribute__((aligned(16))) unsigned long long blockcnt[16];
@@ -323,9 +323,10 @@ __global__ __launch_bounds__(kFusedThreads, (S <= 7 ? 4 : 2)) void k_fused(
         __syncthreads();
         FUSED_STAMP(5);
     }
-    // integer sums commute: one device-scope atomic per counter per block keeps
-    // the totals deterministic and saves the separate k_reduce launch
-    if (tid < C_NUM && blockcnt[tid]) atomicAdd((unsigned long long*)&counters[tid], blockcnt[tid]);
+    // integer sums commute: the block's totals go through the replicated sink
+    // (no k_reduce launch, no single-line atomic hot spot)
+    __syncthreads();
+    if (wv == 0) sink_counters(lane, lane < C_NUM ? blockcnt[lane] : 0, blockIdx.x, gridDim.x, counters, sk);
     FUSED_STAMP_STORE();
 }
 
@@ -355,7 +356,7 @@ __global__ __launch_bounds__(kFusedThreads, ((N - 3) <= 7 ? 4 : 2)) void k_fused
     uint32_t wpb, uint64_t seed, GenSpec gs, uint64_t first_trial, uint64_t batch,
     const uint32_t* __restrict__ faulty, const uint8_t* __restrict__ order,
     uint64_t* __restrict__ decisions, uint8_t* __restrict__ outcome,
-    uint64_t* __restrict__ counters) {
+    uint64_t* __restrict__ counters, Sink sk) {
     using G = Om3<N>;
     constexpr int L = G::L, S = G::S, S1 = G::S1, STRIDE = G::words;
     constexpr uint32_t ME = 3;
@@ -521,10 +522,343 @@ __global__ __launch_bounds__(kFusedThreads, ((N - 3) <= 7 ? 4 : 2)) void k_fused
         __syncthreads();
         FUSED_STAMP(5);
     }
-    // integer sums commute: one device-scope atomic per counter per block keeps
-    // the totals deterministic and saves the separate k_reduce launch
-    if (tid < C_NUM && blockcnt[tid]) atomicAdd((unsigned long long*)&counters[tid], blockcnt[tid]);
+    // integer sums commute: the block's totals go through the replicated sink
+    // (no k_reduce launch, no single-line atomic hot spot)
+    __syncthreads();
+    if (wv == 0) sink_counters(lane, lane < C_NUM ? blockcnt[lane] : 0, blockIdx.x, gridDim.x, counters, sk);
     FUSED_STAMP_STORE();
+}
+
+// ---------------------------------------------------------------------------
+// WAVE engine, effective depth 3: each wave owns W consecutive trial words and
+// resolves them alone (no block barrier anywhere; the 4 waves of a block only
+// share the launch).  The tree is walked one first-hop subtree j1 at a time:
+// a subtree has C = L-1 level-1 slots (j1, a), i.e. C leaf blocks, so lane
+// (w, a), w < W = 64 / C, owns leaf block (j1, a) of word w in every round.
+// For n=10 that is 8 words x 8 leaf blocks = all 64 lanes.  Per round:
+//   1. L1[j1, a] = F[j1] ? lie : L0[j1]            (the lane's own leaf parent)
+//   2. leaf block (j1, a): R2[j1, a, *]             (registers -> LDS, S words)
+//   3. lane (w, b = a): R1[j1, b] = maj(L1[j1, b], R2[j1, a', b] : a' != b),
+//      added into the bit-sliced root counter of receiver column j2(b)
+// R1 is never stored: each root column accumulates as the subtrees finish.
+// Lie bits are keyed exactly as in k_fused3 (level, global slot pair, global
+// word), so both kernels give identical results.
+// LDS per wave (uint64 words): IN[W][N+3] (F[N] OB OO VAL) | L0[W][L] |
+// R2[W][C][S] | RC[W][L][P] (root counters) ; A/U roots reuse R2 when it fits.
+// ---------------------------------------------------------------------------
+// Branch-free synthetic inputs for compile-time N: the same draws as
+// gen_trial (ba_device.hpp), but every Philox call is issued up front and the
+// PK selection steps are predicated, so a lane can carry several trials'
+// chains at once (no data-dependent loop).  Valid for min(f, N) <= PK.
+template <int N, int PK>
+__device__ __forceinline__ void gen_trial_u(uint64_t seed, const GenSpec& g, uint64_t t,
+                                            uint32_t& fmask, uint32_t& oc) {
+    constexpr int CALLS = (2 + PK + 3) / 4;
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    uint32_t u[4 * CALLS];
+    static_for<0, CALLS>([&](auto c) {
+        const P4 b = philox10(P4{(uint32_t)c(), kGenTag, (uint32_t)t, (uint32_t)(t >> 32)}, k0, k1);
+        u[4 * c()] = b.x;
+        u[4 * c() + 1] = b.y;
+        u[4 * c() + 2] = b.z;
+        u[4 * c() + 3] = b.w;
+    });
+    if (g.order_mode == 1) oc = u[0] >> 31;
+    else if (g.order_mode == 2) oc = g.order_value;
+    if (g.faulty_mode != 0) {
+        const uint32_t fcap = g.f < (uint32_t)N ? g.f : (uint32_t)N;
+        const uint32_t nf = g.faulty_mode == 1 ? mulhi_range(u[1], fcap + 1) : fcap;
+        // step i takes the j-th (ascending) general not yet chosen: with the
+        // chosen ones kept sorted (s[0] < s[1] < ...), that general is j plus
+        // the number of chosen positions at or below it, found by one
+        // compare-increment per chosen general in ascending order
+        constexpr int NP = PK < N ? PK : N;
+        uint32_t srt[NP > 0 ? NP : 1];
+        uint32_t mask = 0;
+        static_for<0, NP>([&](auto i) {
+            uint32_t pos = mulhi_range(u[2 + i()], (uint32_t)N - i());
+            static_for<0, i()>([&](auto k) { pos += srt[k()] <= pos ? 1u : 0u; });
+            const bool take = (uint32_t)i() < nf;
+            mask |= take ? (1u << pos) : 0u;
+            // insert pos into the sorted list (an untaken step appends N: sorts last)
+            uint32_t x = take ? pos : (uint32_t)N;
+            static_for<0, i()>([&](auto k) {
+                const uint32_t lo = srt[k()] < x ? srt[k()] : x, hi = srt[k()] < x ? x : srt[k()];
+                srt[k()] = lo;
+                x = hi;
+            });
+            srt[i()] = x;
+        });
+        fmask = mask;
+    }
+}
+
+// Inputs of words [0, W) of a wave task -> bit-sliced words in LDS
+// (in[w*NIN + g] = F[g], then OB, OO, VAL).  PK = 0: the generic gen_trial.
+template <int N, int W, int PK>
+__device__ __forceinline__ void gen_words(uint64_t* in0, uint32_t lane, uint64_t w0, uint64_t seed,
+                                          const GenSpec& gs, uint64_t first_trial, uint64_t batch,
+                                          const uint32_t* __restrict__ faulty,
+                                          const uint8_t* __restrict__ order) {
+    constexpr int NIN = N + 3, G4 = W < 8 ? W : 8;
+    static_for<0, (W + G4 - 1) / G4>([&](auto grp) {
+        constexpr int wb = grp() * G4, nq = W - wb < G4 ? W - wb : G4;
+        uint32_t fm[nq], oc[nq];
+        bool valid[nq];
+        static_for<0, nq>([&](auto q) {
+            const uint64_t i = (w0 + wb + q()) * 64 + lane;
+            valid[q()] = i < batch;
+            fm[q()] = 0;
+            oc[q()] = 0;
+            if (valid[q()]) {
+                if (gs.faulty_mode == 0) fm[q()] = faulty[i];
+                if (gs.order_mode == 0) oc[q()] = order[i];
+                if constexpr (PK > 0) gen_trial_u<N, PK>(seed, gs, first_trial + i, fm[q()], oc[q()]);
+                else gen_trial(N, seed, gs, first_trial + i, fm[q()], oc[q()]);
+            }
+        });
+        static_for<0, nq>([&](auto q) {
+            uint64_t mine = 0;
+            static_for<0, N>([&](auto g) {
+                const uint64_t b = __ballot(valid[q()] && ((fm[q()] >> g()) & 1u));
+                if (lane == g()) mine = b;
+            });
+            const uint64_t ob = __ballot(valid[q()] && oc[q()] == 1);
+            const uint64_t oo = __ballot(valid[q()] && oc[q()] == 2);
+            const uint64_t vv = __ballot(valid[q()]);
+            uint64_t* in = in0 + (wb + q()) * NIN;
+            if (lane < (uint32_t)N) in[lane] = mine;
+            if (lane == 0) {
+                in[N] = ob;
+                in[N + 1] = oo;
+                in[N + 2] = vv;
+            }
+        });
+    });
+}
+
+template <int N>
+struct Om3W {
+    static constexpr int L = N - 1, S = N - 3, C = L - 1;
+    static constexpr int W = 64 / C;               // trial words per wave task
+    static constexpr int LANES = W * C;            // lanes busy in the subtree rounds
+    static constexpr int P = planes_c(L);          // root counter planes (L inputs)
+    static constexpr int NIN = N + 3;
+    static constexpr int oIN = 0, oL0 = oIN + W * NIN, oR2 = oL0 + W * L, oRC = oR2 + W * C * S;
+    static constexpr int end0 = oRC + W * L * P;
+    static constexpr bool au_in_r2 = 2 * L <= C * S;
+    static constexpr int oAU = au_in_r2 ? oR2 : end0;
+    static constexpr int words = ((au_in_r2 ? end0 : end0 + W * 2 * L) + 1) & ~1;
+};
+
+// DIAG: lab-only ablation switches (tools/om3_lab.hip); the product uses 0.
+template <int N, int DIAG = 0>
+__global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
+    uint64_t seed, GenSpec gs, uint64_t first_trial, uint64_t batch,
+    const uint32_t* __restrict__ faulty, const uint8_t* __restrict__ order,
+    uint64_t* __restrict__ decisions, uint8_t* __restrict__ outcome,
+    uint64_t* __restrict__ counters, Sink sk) {
+    using G = Om3W<N>;
+    constexpr int L = G::L, S = G::S, C = G::C, W = G::W, P = G::P, NIN = G::NIN;
+    constexpr uint32_t ME = 3;
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    uint64_t* img = lds + (uint64_t)wv * G::words;
+    const uint64_t total_words = (batch + 63) / 64;
+    const uint64_t ntasks = (total_words + W - 1) / W;
+    // this lane's (word, leaf block) in the subtree rounds
+    const uint32_t lw_ = lane / C, la = lane - lw_ * C;
+    const bool act = lane < (uint32_t)G::LANES;
+    const uint32_t lw = act ? lw_ : 0;
+    TrialCounts tc;
+    FUSED_STAMP_INIT();
+#ifdef BA_FUSED_STAMPS
+    const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    for (uint64_t task = (uint64_t)blockIdx.x * wpb + wv; task < ntasks;
+         task += (uint64_t)gridDim.x * wpb) {
+        const uint64_t w0 = task * W;
+        const uint64_t gw0 = (first_trial >> 6) + w0;
+        // ---- inputs -> bit-sliced words (four words' draws in flight per lane) ---
+        {
+            const uint32_t pk = gs.faulty_mode == 0 ? 0u : (gs.f < (uint32_t)N ? gs.f : (uint32_t)N);
+            uint64_t* in0 = img + G::oIN;
+            if (pk <= 2) gen_words<N, W, 2>(in0, lane, w0, seed, gs, first_trial, batch, faulty, order);
+            else if (pk <= 3) gen_words<N, W, 3>(in0, lane, w0, seed, gs, first_trial, batch, faulty, order);
+            else if (pk <= 6) gen_words<N, W, 6>(in0, lane, w0, seed, gs, first_trial, batch, faulty, order);
+            else gen_words<N, W, 0>(in0, lane, w0, seed, gs, first_trial, batch, faulty, order);
+        }
+        __builtin_amdgcn_wave_barrier();
+        FUSED_STAMP(0);
+        // ---- level 0 (one Philox per slot pair) and root counter init -----------
+        {
+            constexpr uint32_t NP0 = (L + 1) / 2;
+            for (uint32_t it = lane; it < (uint32_t)W * NP0; it += 64) {
+                const uint32_t w = it / NP0, p = it - w * NP0;
+                const uint64_t* in = img + G::oIN + w * NIN;
+                const uint64_t F0 = in[0], ob = in[N];
+                uint64_t l0[2];
+                lie_pair(seed, 0, p, gw0 + w, l0[0], l0[1]);
+                static_for<0, 2>([&](auto h) {
+                    const uint32_t j = 2 * p + h();
+                    if (j < (uint32_t)L) {
+                        const uint64_t v = (F0 & l0[h()]) | (~F0 & ob);
+                        img[G::oL0 + w * L + j] = v;
+                        uint64_t* rc = img + G::oRC + (w * L + j) * P;
+                        rc[0] = v;
+                        static_for<1, P>([&](auto q) { rc[q()] = 0; });
+                    }
+                });
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // ---- subtree rounds ------------------------------------------------------
+        const uint64_t* in = img + G::oIN + lw * NIN;
+        const uint64_t gw = gw0 + lw;
+        for (uint32_t j1 = 0; j1 < (uint32_t)L; ++j1) {
+            if constexpr ((DIAG & 8) == 0) {
+                // alternate the issue priority of the waves sharing a SIMD each
+                // round (wave slot parity): with equal priority the older wave
+                // takes nearly every VALU slot and the younger one finishes its
+                // task alone at single-wave issue rate (tools/om3_lab: -7%)
+                const uint32_t slot = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (3 << 11)) & 1u;
+                if (((j1 + slot) & 1u) != 0) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            }
+            const uint32_t sr = j1 * C + la;             // level-1 slot (j1, j2)
+            const uint32_t j2 = la + (la >= j1);
+            uint64_t par = 0;
+            if (act) {
+                // 1. L1[j1, a]: sender j1 relays L0[j1]
+                uint64_t l1[2];
+                lie_pair(seed, 1, sr >> 1, gw, l1[0], l1[1]);
+                const uint64_t lie = (sr & 1u) ? l1[1] : l1[0];
+                const uint64_t fj = in[j1 + 1];
+                par = (fj & lie) | (~fj & img[G::oL0 + lw * L + j1]);
+                // 2. leaf block (j1, a): level-2 diagonal, then S(S-1) leaves
+                const uint32_t lo = j1 < j2 ? j1 : j2, hi = j1 < j2 ? j2 : j1;
+                const uint64_t fs = in[j2 + 1];  // level-2 sender: j2
+                const uint32_t x0 = sr * S;
+                constexpr int NPD = (S + 1) / 2;
+                uint64_t lw2[2 * NPD];
+                static_for<0, NPD>([&](auto qd) {
+                    lie_pair(seed, 2, (x0 >> 1) + qd(), gw, lw2[2 * qd()], lw2[2 * qd() + 1]);
+                });
+                const uint64_t oddmask = 0ull - (uint64_t)(x0 & 1u);
+                uint64_t diag[S], Fm[S], R[S];
+                static_for<0, S>([&](auto a) {
+                    uint64_t lie2;
+                    if constexpr (S % 2 == 1) lie2 = lw2[a()] ^ ((lw2[a()] ^ lw2[a() + 1]) & oddmask);
+                    else lie2 = lw2[a()];
+                    diag[a()] = (fs & lie2) | (~fs & par);
+                    const uint32_t ida = a() + (a() >= lo) + (a() + 1 >= hi);  // member a's rank
+                    Fm[a()] = in[ida + 1];
+                });
+                leaf_block<S>(ME, seed, gw, sr, diag, Fm, R);
+                uint64_t* r2 = img + G::oR2 + (lw * C + la) * S;
+                static_for<0, S>([&](auto d) { r2[d()] = R[d()]; });
+            }
+            __builtin_amdgcn_wave_barrier();
+            FUSED_STAMP(1);
+            if (act) {
+                // 3. R1[j1, b], b = la: L1[j1, b] (this lane's own parent) plus
+                //    column b of the word's other leaf blocks a' != b
+                const uint32_t b = la;
+                Count<planes_c(C)> cnt;
+                cnt.add(par);
+                const uint64_t* r2w = img + G::oR2 + lw * C * S;
+                static_for<0, C>([&](auto a) {
+                    if (a() == b) return;
+                    cnt.add(r2w[a() * S + (a() < b ? b - 1 : b)]);
+                });
+                const uint64_t r1 = cnt.ge(C / 2 + 1);  // inner tie -> non-attack
+                // root column j2 += R1[j1, b] (ripple add on the bit-sliced planes)
+                uint64_t* rc = img + G::oRC + (lw * L + j2) * P;
+                uint64_t x = r1;
+                static_for<0, P>([&](auto q) {
+                    const uint64_t c = rc[q()];
+                    rc[q()] = c ^ x;
+                    x &= c;
+                });
+            }
+            __builtin_amdgcn_wave_barrier();
+            FUSED_STAMP(2);
+        }
+        // ---- roots: strict majority, tie -> undefined ----------------------------
+        for (uint32_t it = lane; it < (uint32_t)W * L; it += 64) {
+            const uint32_t w = it / L, col = it - w * L;
+            const uint64_t* rc = img + G::oRC + (w * L + col) * P;
+            Count<P> cnt;
+            static_for<0, P>([&](auto q) { cnt.c[q()] = rc[q()]; });
+            const uint64_t att = cnt.ge(L / 2 + 1);
+            const uint64_t tie = (L & 1) ? 0ull : (cnt.ge(L / 2) & ~att);
+            img[G::oAU + w * 2 * L + col] = att;
+            img[G::oAU + w * 2 * L + L + col] = tie;
+        }
+        __builtin_amdgcn_wave_barrier();
+        FUSED_STAMP(3);
+        // ---- per-trial epilogue: lane = trial, all W words unrolled (branch-free
+        //      except the stores, so the words' LDS reads and logic interleave) --
+        static_for<0, W>([&](auto wq) {
+            constexpr int w = wq();
+            const uint64_t* inw = img + G::oIN + w * NIN;
+            const uint64_t* au = img + G::oAU + w * 2 * L;
+            const uint64_t i = (w0 + w) * 64 + lane;
+            const bool live = (inw[N + 2] >> lane) & 1ull;
+            uint32_t A = 0, U = 0, fm = 0;
+            static_for<0, L>([&](auto b) {
+                A |= (uint32_t)((au[b()] >> lane) & 1ull) << (b() + 1);
+                U |= (uint32_t)((au[L + b()] >> lane) & 1ull) << (b() + 1);
+            });
+            static_for<0, N>([&](auto g) { fm |= (uint32_t)((inw[g()] >> lane) & 1ull) << g(); });
+            const uint32_t ob = (uint32_t)(inw[N] >> lane) & 1u;
+            const uint32_t oo = (uint32_t)(inw[N + 1] >> lane) & 1u;
+            const TrialResult r = trial_result(N, ME, fm, oo ? 2u : ob, A, U);
+            const uint32_t lv = live ? 1u : 0u;
+            const uint32_t q = r.out & 3, agree = (r.out >> 2) & 1, appl = (r.out >> 3) & 1;
+            const uint32_t valid = (r.out >> 4) & 1, inb = (r.out >> 5) & 1;
+            tc.v[C_TRIALS] += lv;
+            tc.v[C_AGREE] += lv & agree;
+            tc.v[C_VAPPL] += lv & appl;
+            tc.v[C_VALID] += lv & valid;
+            tc.v[C_QR] += lv & (q == 0);
+            tc.v[C_QA] += lv & (q == 1);
+            tc.v[C_QU] += lv & (q == 2);
+            tc.v[C_UNDEF] += lv * r.nU;
+            tc.v[C_INB] += lv & inb;
+            tc.v[C_VIOL] += lv & inb & ((agree ^ 1u) | (appl & (valid ^ 1u)));
+            tc.v[C_FTOT] += lv * r.nf;
+            tc.v[C_ATT] += lv * r.nA;
+            if (live) {
+                if (!(DIAG & 1) && decisions) decisions[i] = r.dec;
+                if (!(DIAG & 2) && outcome) outcome[i] = (uint8_t)r.out;
+            }
+        });
+        __builtin_amdgcn_wave_barrier();
+        FUSED_STAMP(4);
+    }
+    // run counters: wave sums (lane c holds counter c) into the replicated sink
+    uint64_t mine = 0;
+#pragma unroll
+    for (int c = 0; c < C_NUM; ++c) {
+        uint32_t x = tc.v[c];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+        if (lane == (uint32_t)c) mine = x;
+    }
+    if (!(DIAG & 4)) sink_counters(lane, mine, blockIdx.x * wpb + wv, gridDim.x * wpb, counters, sk);
+#ifdef BA_FUSED_STAMPS
+    if (lane == 0 && blockIdx.x * wpb + wv < (uint32_t)kPartialRows)
+    {
+        for (int i = 0; i < 6; ++i) g_fused_stamps[blockIdx.x * wpb + wv][i] = st_acc[i];
+        g_fused_stamps[blockIdx.x * wpb + wv][6] = rt0;
+        // [5]: HW_ID | XCC_ID << 32 (s_getreg: id | offset << 6 | (size - 1) << 11)
+        g_fused_stamps[blockIdx.x * wpb + wv][5] =
+            __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11)) |
+            ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (31 << 11)) << 32);
+        g_fused_stamps[blockIdx.x * wpb + wv][7] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -618,16 +952,51 @@ static void launch_fused_s(const FusedPlan& fp, const FusedPlan* d_fp, uint32_t 
                            uint64_t* partials) {
     hipLaunchKernelGGL(k_fused<S>, dim3(blocks), dim3(fp.threads), lds_bytes, a.stream, d_fp,
                        a.seed, a.gen, a.first_trial, a.batch, a.faulty, a.order, d_sender, a.members,
-                       a.decisions, a.outcome, a.counters);
+                       a.decisions, a.outcome, a.counters, a.sink);
+}
+
+// WAVE engine launch: one wave per W-word task, 4 independent waves per block,
+// at most two blocks per CU (the kernel's registers allow three, but two waves
+// per SIMD with whole tasks each balance best) and a persistent task loop.
+template <int N>
+static hipError_t launch_om3w_n(const RunArgs& a) {
+    using G = Om3W<N>;
+    constexpr uint32_t wpb = kWaveThreads / 64;
+    const uint64_t words = (a.batch + 63) / 64, tasks = (words + G::W - 1) / G::W;
+    uint64_t blocks = (tasks + wpb - 1) / wpb;
+    uint64_t cap = 2ull * a.cu_count;
+    if (const char* e = getenv("BA_WAVE_MAX_BLOCKS")) {  // tests: force the persistent task loop
+        const uint64_t c = strtoull(e, nullptr, 0);
+        if (c >= 1 && c < cap) cap = c;
+    }
+    if (blocks > cap) blocks = cap;
+    ProfScope ps(a.prof, "k_om3w", a.stream);
+    hipLaunchKernelGGL(k_om3w<N>, dim3((uint32_t)blocks), dim3(kWaveThreads), wpb * G::words * 8,
+                       a.stream, a.seed, a.gen, a.first_trial, a.batch, a.faulty, a.order,
+                       a.decisions, a.outcome, a.counters, a.sink);
+    return hipGetLastError();
 }
 
 hipError_t launch_fused(const RunArgs& a, const Geometry& g, const FusedPlan& fp,
                         const FusedPlan* d_fp, const uint8_t* d_sender, uint64_t* partials) {
     const uint64_t words = (a.batch + 63) / 64;
-    // effective depth 3 with 5 <= n <= 14 runs the compile-time-specialised
-    // kernel (BA_FUSED_GENERIC=1 forces the generic one, for cross-checks)
-    static const bool force_generic = getenv("BA_FUSED_GENERIC") && atoi(getenv("BA_FUSED_GENERIC")) == 1;
-    const bool spec3 = g.me == 3 && g.n >= 5 && g.n <= 14 && !force_generic;
+    // effective depth 3, 5 <= n <= 14: the WAVE kernel k_om3w.  BA_FUSED_KIND
+    // selects the alternatives for cross-checks: 1 = block kernel k_fused3,
+    // 2 = generic k_fused.
+    const char* kenv = getenv("BA_FUSED_KIND");
+    const int kind = kenv ? atoi(kenv) : 0;
+    if (g.me == 3 && g.n >= 5 && g.n <= 14 && kind == 0) {
+        switch (g.n) {
+#define OM3W_CASE(nn) \
+    case nn: return launch_om3w_n<nn>(a);
+            OM3W_CASE(5) OM3W_CASE(6) OM3W_CASE(7) OM3W_CASE(8) OM3W_CASE(9) OM3W_CASE(10)
+            OM3W_CASE(11) OM3W_CASE(12) OM3W_CASE(13) OM3W_CASE(14)
+#undef OM3W_CASE
+            default: return hipErrorInvalidValue;
+        }
+    }
+    // BA_FUSED_KIND=1: the compile-time-specialised block kernel k_fused3
+    const bool spec3 = g.me == 3 && g.n >= 5 && g.n <= 14 && kind != 2;
     // one block per resident slot (occupancy x CUs): each owns an equal run of words
     int occ = 0;
     if (spec3) {
@@ -672,7 +1041,7 @@ hipError_t launch_fused(const RunArgs& a, const Geometry& g, const FusedPlan& fp
     case nn:                                                                                     \
         hipLaunchKernelGGL(k_fused3<nn>, dim3(blocks), dim3(kFusedThreads), lds_bytes, a.stream, \
                            fp.wpb, a.seed, a.gen, a.first_trial, a.batch, a.faulty, a.order,     \
-                           a.decisions, a.outcome, a.counters);                                 \
+                           a.decisions, a.outcome, a.counters, a.sink);                         \
         break;
                 FUSED3_CASE(5) FUSED3_CASE(6) FUSED3_CASE(7) FUSED3_CASE(8) FUSED3_CASE(9)
                 FUSED3_CASE(10) FUSED3_CASE(11) FUSED3_CASE(12) FUSED3_CASE(13) FUSED3_CASE(14)

@@ -15,7 +15,10 @@
  *   - Host-pointer entry points copy in/out over PCIe; *_device entry points
  *     take device pointers and a hipStream_t (as void*) and are asynchronous.
  *   - One ctx per host thread; a ctx is not thread-safe.  The library owns
- *     the device scratch it allocates inside the ctx.
+ *     the device scratch it allocates inside the ctx (including the run
+ *     counter reduction slots), so the *_device calls of one ctx must be
+ *     stream-ordered: do not let two of them run concurrently on different
+ *     streams (use one ctx per concurrent stream).
  *
  * General indexing: the live generals sorted by id are
  * indexed 0..n-1; index 0 is the commander (lowest live id, ba.py:381 +

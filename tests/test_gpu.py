@@ -275,3 +275,47 @@ def test_philox_om1_equals_table_mode_gpu(engine, n):
     same(res_p.decisions, res_t.decisions, "decisions")
     same(res_p.outcome, res_t.outcome, "outcome")
     assert res_p.counters == res_t.counters
+
+
+# --- effective depth 3: the WAVE kernel vs the block and generic FUSED kernels --
+OM3_CASES = [(5, 3, 1, 1), (5, 4, 2, 1), (6, 3, 1, 2), (7, 3, 2, 1), (8, 3, 3, 1), (9, 3, 3, 2),
+             (10, 3, 0, 1), (10, 3, 3, 1), (10, 3, 5, 2), (10, 3, 10, 1), (11, 3, 4, 1),
+             (12, 3, 7, 2), (13, 3, 4, 1), (14, 3, 14, 2), (14, 3, 4, 0)]
+
+
+@pytest.mark.parametrize("n,m,f,fmode", OM3_CASES)
+def test_om3_wave_block_generic_vs_oracle(monkeypatch, n, m, f, fmode):
+    """k_om3w (default), k_fused3 (BA_FUSED_KIND=1) and k_fused (=2) against the
+    oracle, over every synthetic-input path of the WAVE kernel's branch-free
+    generator (f <= 2, 3, <= 6 and the generic fallback; random / exact /
+    given faulty sets), a ragged batch, and the persistent task loop
+    (BA_WAVE_MAX_BLOCKS=1: four waves walk all tasks)."""
+    from ba_amd import lib as L
+    B = 64 * 8 * 5 + 37
+    if fmode == 0:
+        rng = np.random.default_rng(n * 31 + f)
+        fm = (rng.integers(0, 1 << n, B, dtype=np.uint64) & rng.integers(0, 1 << n, B, dtype=np.uint64)
+              ).astype(np.uint32)
+        oc = rng.choice([0, 1, 2], B).astype(np.uint8)
+        kw = dict(seed=7, faulty=fm, order=oc, first_trial=64 * 3)
+        ref = oracle_c.run(n, m, B, seed=7, faulty=fm, order=oc, first_trial=64 * 3)
+    else:
+        kw = dict(seed=0xBA5EED + n, faulty_mode=fmode, f=f, order_mode=L.ORDER_RANDOM if f % 2 else
+                  L.ORDER_CONST, order_value=1, first_trial=64 * 77)
+        ref = oracle_c.run(n, m, B, **kw)
+    od, oo, ocnt = ref
+    for kind, cap in (("0", None), ("0", "1"), ("1", None), ("2", None)):
+        monkeypatch.setenv("BA_FUSED_KIND", kind)
+        if cap:
+            monkeypatch.setenv("BA_WAVE_MAX_BLOCKS", cap)
+        else:
+            monkeypatch.delenv("BA_WAVE_MAX_BLOCKS", raising=False)
+        e = L.Engine(0)
+        try:
+            res = e.run(n, m, B, engine=L.ENGINE_FUSED, **kw)
+        finally:
+            e.close()
+        tag = f"kind={kind} cap={cap} n={n} m={m} f={f} fmode={fmode}"
+        same(res.decisions, od, "decisions " + tag)
+        same(res.outcome, oo, "outcome " + tag)
+        assert {k: res.counters[k] for k in ocnt} == ocnt, tag
