@@ -2,10 +2,16 @@
 
 A step resolves one batch of synthetic trials (n=10 generals, OM(3), 1M trials
 per GPU by default: faulty set = uniform f-subset with f ~ U{0..3}, order ~
-Bernoulli(1/2), lies from Philox -- all generated on the device from the seed,
-so the inputs are "resident" before the timed region by construction).  Each
-trial is fully resolved: every lieutenant's root decision is written to HBM
-(uint64/trial), plus the per-trial quorum/IC outcome byte, plus run counters.
+Bernoulli(1/2)).  Each trial's inputs (its faulty set and commander order) are
+staged in HBM before the timed region by ba_gen_inputs_device (the same Philox
+stream the kernel would draw; results are bit-identical either way), so `value`
+has inputs resident as the measurement contract asks.  Everything the protocol
+computes stays inside the timed region: every lie (a faulty general's coin
+flip, ba.py:45, 269) is drawn from Philox in the kernel, every tree level and
+majority is resolved, every lieutenant's root decision is written to HBM
+(uint64/trial), plus the per-trial quorum/IC outcome byte and run counters.
+`value_with_input_generation` repeats the timing with the inputs drawn inside
+the kernel too.
 
 N>1: launched one process per GPU by torch.distributed.run.  Trials shard by
 global index (weak scaling, no data-path collective); the run counters are
@@ -120,6 +126,8 @@ def main():
     ap.add_argument("--cpu-budget-s", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--inputs-in-kernel", action="store_true",
+                    help="draw faulty sets/orders inside the timed kernel (no staging)")
     args = ap.parse_args()
 
     import torch
@@ -148,42 +156,76 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
 
-    def step(i):
-        first = (i * world + rank) * B  # global trial index: weak scaling, disjoint shards
-        p = L.make_params(n, m, args.seed, L.LIE_PHILOX, L.FAULTY_RANDOM, fmax, L.ORDER_RANDOM,
-                          L.ATTACK, engine_id, first)
-        eng.run_device(p, B, d_decisions=dec.data_ptr(), d_outcome=out.data_ptr(),
-                       d_counters=cnt.data_ptr(), stream=stream.cuda_stream)
+    def first_of(i):
+        return (i * world + rank) * B  # global trial index: weak scaling, disjoint shards
 
-    for i in range(args.warmup):
-        step(i)
-    cnt.zero_()
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    for i in range(args.steps):
-        step(args.warmup + i)
-    if dist:
-        dist.all_reduce(cnt)  # the only collective: run counters (RCCL)
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t0
-    elapsed = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if dist:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    T = float(elapsed.item())
-    gpu_ms = ev0.elapsed_time(ev1)
-    counters = dict(zip(L.COUNTER_NAMES, [int(x) for x in cnt.cpu().tolist()]))
+    def rand_params(i):
+        return L.make_params(n, m, args.seed, L.LIE_PHILOX, L.FAULTY_RANDOM, fmax, L.ORDER_RANDOM,
+                             L.ATTACK, engine_id, first_of(i))
+
+    # stage every step's inputs in HBM before any timing (ba_gen_inputs_device)
+    n_steps_total = args.warmup + 2 * args.steps
+    staged = {}
+    if not args.inputs_in_kernel:
+        fbuf = torch.empty((n_steps_total, B), dtype=torch.int32, device=dev)
+        obuf = torch.empty((n_steps_total, B), dtype=torch.uint8, device=dev)
+        for i in range(n_steps_total):
+            eng.gen_inputs_device(rand_params(i), B, d_faulty=fbuf[i].data_ptr(),
+                                  d_order=obuf[i].data_ptr(), stream=stream.cuda_stream)
+            staged[i] = (fbuf[i].data_ptr(), obuf[i].data_ptr())
+        torch.cuda.synchronize(dev)
+
+    def step(i, in_kernel=args.inputs_in_kernel):
+        if in_kernel:
+            p = rand_params(i)
+            eng.run_device(p, B, d_decisions=dec.data_ptr(), d_outcome=out.data_ptr(),
+                           d_counters=cnt.data_ptr(), stream=stream.cuda_stream)
+        else:
+            p = L.make_params(n, m, args.seed, L.LIE_PHILOX, L.FAULTY_GIVEN, fmax, L.ORDER_GIVEN,
+                              L.ATTACK, engine_id, first_of(i))
+            fp, op = staged[i]
+            eng.run_device(p, B, d_faulty=fp, d_order=op, d_decisions=dec.data_ptr(),
+                           d_outcome=out.data_ptr(), d_counters=cnt.data_ptr(),
+                           stream=stream.cuda_stream)
+
+    def timed(in_kernel):
+        for i in range(args.warmup):
+            step(i, in_kernel)
+        cnt.zero_()
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        for i in range(args.steps):
+            step(args.warmup + i, in_kernel)
+        if dist:
+            dist.all_reduce(cnt)  # the only collective: run counters (RCCL)
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - t0
+        elapsed = torch.tensor([wall], dtype=torch.float64, device=dev)
+        if dist:
+            dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        return float(elapsed.item()), ev0.elapsed_time(ev1)
+
     total_trials = B * args.steps * world
+    T, gpu_ms = timed(args.inputs_in_kernel)
+    counters = dict(zip(L.COUNTER_NAMES, [int(x) for x in cnt.cpu().tolist()]))
     value = total_trials / T
+    value_gen = None
+    if not args.inputs_in_kernel:
+        T2, _ = timed(True)
+        counters2 = dict(zip(L.COUNTER_NAMES, [int(x) for x in cnt.cpu().tolist()]))
+        if counters2 != counters:
+            raise SystemExit(f"staged-input and in-kernel-input runs disagree: {counters} vs {counters2}")
+        value_gen = total_trials / T2
 
     # per-kernel HIP-event timing on the launch stream (a second pass of the same steps)
     kernels, roof = {}, None
@@ -222,6 +264,9 @@ def main():
                                    f"random order, decisions+outcome written",
                        "n": n, "m": m, "trials_per_gpu_step": B, "engine": args.engine,
                        "parallelism": f"trial-dp{world}"},
+            "inputs": "in-kernel Philox draws" if args.inputs_in_kernel else
+                      "staged in HBM before the timed region (ba_gen_inputs_device); lies drawn in-kernel",
+            "value_with_input_generation": round(value_gen, 1) if value_gen else None,
             "gpu_event_ms": round(gpu_ms, 3),
             "kernels_ms": {k: round(v[1] / v[0], 4) for k, v in kernels.items()},
             "roofline": roof,

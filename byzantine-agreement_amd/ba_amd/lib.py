@@ -35,7 +35,7 @@ EXPORTS = ["ba_version", "ba_device_count", "ba_ctx_create", "ba_ctx_destroy", "
            "ba_run_trials", "ba_run_trials_device", "ba_tree_slots", "ba_level_slots",
            "ba_engine_for", "ba_profile_enable", "ba_profile_read", "ba_mt_seed", "ba_mt_next32",
            "ba_om1_coin_count", "ba_mt_draw_coins", "ba_mt_table", "ba_vote_slots",
-           "ba_subtree_votes_device", "ba_root_from_votes_device"]
+           "ba_subtree_votes_device", "ba_root_from_votes_device", "ba_gen_inputs_device"]
 
 
 class BAError(RuntimeError):
@@ -95,6 +95,7 @@ def load(path: str | None = None):
                                   ctypes.POINTER(Counters)]
     lib.ba_run_trials_device.argtypes = [vp, ctypes.POINTER(Params), u64, vp, vp, vp, vp, vp,
                                          vp, vp, vp]
+    lib.ba_gen_inputs_device.argtypes = [vp, ctypes.POINTER(Params), u64, vp, vp, vp]
     lib.ba_tree_slots.argtypes = [u32, u32]
     lib.ba_tree_slots.restype = u64
     lib.ba_level_slots.argtypes = [u32, u32, u32]
@@ -235,6 +236,12 @@ class Engine:
             self.handle, ctypes.byref(params), batch, d_faulty or None, d_order or None,
             d_table or None, d_poll or None, d_decisions or None, d_outcome or None,
             d_counters or None, stream or None))
+
+    def gen_inputs_device(self, params: Params, batch: int, d_faulty=0, d_order=0, stream=0):
+        """Stage the synthetic faulty sets / orders of a batch in HBM (see include/ba.h)."""
+        _check(self.lib, self.lib.ba_gen_inputs_device(
+            self.handle, ctypes.byref(params), batch, d_faulty or None, d_order or None,
+            stream or None))
 
     def subtree_votes_device(self, params: Params, batch: int, j_begin: int, j_end: int,
                              d_votes: int, d_faulty=0, d_order=0, stream=0):

@@ -538,6 +538,23 @@ extern "C" int ba_run_trials_device(ba_ctx* ctx, const ba_params* p, uint64_t ba
     return run_levels(ctx, a, ge, LevelsJob{}, 0, g.L, false, partials);
 }
 
+extern "C" int ba_gen_inputs_device(ba_ctx* ctx, const ba_params* p, uint64_t batch,
+                                    uint32_t* d_faulty, uint8_t* d_order, void* stream) {
+    if (!ctx) return fail(BA_EINVAL, "ctx is NULL");
+    int rc = validate(p, batch, true, true, false);
+    if (rc != BA_OK) return rc;
+    if (d_faulty && p->faulty_mode == BA_FAULTY_GIVEN)
+        return fail(BA_EINVAL, "faulty_mode is GIVEN: no faulty sets to generate");
+    if (d_order && p->order_mode == BA_ORDER_GIVEN)
+        return fail(BA_EINVAL, "order_mode is GIVEN: no orders to generate");
+    if (batch == 0 || (!d_faulty && !d_order)) return BA_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    RunArgs a = make_args(ctx, p, batch, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                          nullptr, stream);
+    HIP_TRY(launch_gen_inputs(a, d_faulty, d_order));
+    return BA_OK;
+}
+
 extern "C" uint64_t ba_vote_slots(uint32_t n, uint32_t m, uint32_t j_begin, uint32_t j_end) {
     if (n < 3 || n > BA_MAX_GENERALS || effective_depth(n, m) == 0) return 0;
     if (j_begin > j_end || j_end > n - 1) return 0;

@@ -126,6 +126,7 @@ hipError_t launch_fused(const RunArgs& a, const Geometry& g, const FusedPlan& fp
                         const FusedPlan* d_fp, const uint8_t* d_sender, uint64_t* partials);
 
 hipError_t launch_table(const RunArgs& a, uint64_t* partials);
+hipError_t launch_gen_inputs(const RunArgs& a, uint32_t* faulty_out, uint8_t* order_out);
 hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_t* d_sender,
                                uint64_t* scratch, const LevelsLayout& lay, uint64_t trial0,
                                uint64_t ntrials, uint64_t* partials, const LevelsJob& job);

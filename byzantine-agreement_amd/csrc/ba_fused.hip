@@ -547,12 +547,14 @@ __global__ __launch_bounds__(kFusedThreads, ((N - 3) <= 7 ? 4 : 2)) void k_fused
 // R2[W][C][S] | RC[W][L][P] (root counters) ; A/U roots reuse R2 when it fits.
 // ---------------------------------------------------------------------------
 // Branch-free synthetic inputs for compile-time N: the same draws as
-// gen_trial (ba_device.hpp), but every Philox call is issued up front and the
-// PK selection steps are predicated, so a lane can carry several trials'
-// chains at once (no data-dependent loop).  Valid for min(f, N) <= PK.
+// gen_trial (ba_device.hpp), but every Philox call is issued up front, the
+// PK selection steps are predicated and the modes are selects, so the code
+// for several trials is one basic block and their chains interleave.  fm / oc
+// carry the given values in and the resolved ones out.  Valid for
+// min(f, N) <= PK.
 template <int N, int PK>
 __device__ __forceinline__ void gen_trial_u(uint64_t seed, const GenSpec& g, uint64_t t,
-                                            uint32_t& fmask, uint32_t& oc) {
+                                            uint32_t& fm, uint32_t& oc) {
     constexpr int CALLS = (2 + PK + 3) / 4;
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     uint32_t u[4 * CALLS];
@@ -563,38 +565,36 @@ __device__ __forceinline__ void gen_trial_u(uint64_t seed, const GenSpec& g, uin
         u[4 * c() + 2] = b.z;
         u[4 * c() + 3] = b.w;
     });
-    if (g.order_mode == 1) oc = u[0] >> 31;
-    else if (g.order_mode == 2) oc = g.order_value;
-    if (g.faulty_mode != 0) {
-        const uint32_t fcap = g.f < (uint32_t)N ? g.f : (uint32_t)N;
-        const uint32_t nf = g.faulty_mode == 1 ? mulhi_range(u[1], fcap + 1) : fcap;
-        // step i takes the j-th (ascending) general not yet chosen: with the
-        // chosen ones kept sorted (s[0] < s[1] < ...), that general is j plus
-        // the number of chosen positions at or below it, found by one
-        // compare-increment per chosen general in ascending order
-        constexpr int NP = PK < N ? PK : N;
-        uint32_t srt[NP > 0 ? NP : 1];
-        uint32_t mask = 0;
-        static_for<0, NP>([&](auto i) {
-            uint32_t pos = mulhi_range(u[2 + i()], (uint32_t)N - i());
-            static_for<0, i()>([&](auto k) { pos += srt[k()] <= pos ? 1u : 0u; });
-            const bool take = (uint32_t)i() < nf;
-            mask |= take ? (1u << pos) : 0u;
-            // insert pos into the sorted list (an untaken step appends N: sorts last)
-            uint32_t x = take ? pos : (uint32_t)N;
-            static_for<0, i()>([&](auto k) {
-                const uint32_t lo = srt[k()] < x ? srt[k()] : x, hi = srt[k()] < x ? x : srt[k()];
-                srt[k()] = lo;
-                x = hi;
-            });
-            srt[i()] = x;
+    oc = g.order_mode == 1 ? u[0] >> 31 : (g.order_mode == 2 ? g.order_value : oc);
+    const uint32_t fcap = g.f < (uint32_t)N ? g.f : (uint32_t)N;
+    const uint32_t nf = g.faulty_mode == 1 ? mulhi_range(u[1], fcap + 1) : fcap;
+    // step i takes the j-th (ascending) general not yet chosen: with the
+    // chosen ones kept sorted (s[0] < s[1] < ...), that general is j plus the
+    // number of chosen positions at or below it, found by one compare-increment
+    // per chosen general in ascending order
+    constexpr int NP = PK < N ? PK : N;
+    uint32_t srt[NP > 0 ? NP : 1];
+    uint32_t mask = 0;
+    static_for<0, NP>([&](auto i) {
+        uint32_t pos = mulhi_range(u[2 + i()], (uint32_t)N - i());
+        static_for<0, i()>([&](auto k) { pos += srt[k()] <= pos ? 1u : 0u; });
+        const bool take = (uint32_t)i() < nf;
+        mask |= take ? (1u << pos) : 0u;
+        // insert pos into the sorted list (an untaken step appends N: sorts last)
+        uint32_t x = take ? pos : (uint32_t)N;
+        static_for<0, i()>([&](auto k) {
+            const uint32_t lo = srt[k()] < x ? srt[k()] : x, hi = srt[k()] < x ? x : srt[k()];
+            srt[k()] = lo;
+            x = hi;
         });
-        fmask = mask;
-    }
+        srt[i()] = x;
+    });
+    fm = g.faulty_mode != 0 ? mask : fm;
 }
 
 // Inputs of words [0, W) of a wave task -> bit-sliced words in LDS
-// (in[w*NIN + g] = F[g], then OB, OO, VAL).  PK = 0: the generic gen_trial.
+// (in[w*NIN + g] = F[g], then OB, OO, VAL).  PK = 0: the generic gen_trial;
+// PK = -1: both inputs given (loads only).
 template <int N, int W, int PK>
 __device__ __forceinline__ void gen_words(uint64_t* in0, uint32_t lane, uint64_t w0, uint64_t seed,
                                           const GenSpec& gs, uint64_t first_trial, uint64_t batch,
@@ -605,16 +605,26 @@ __device__ __forceinline__ void gen_words(uint64_t* in0, uint32_t lane, uint64_t
         constexpr int wb = grp() * G4, nq = W - wb < G4 ? W - wb : G4;
         uint32_t fm[nq], oc[nq];
         bool valid[nq];
+        // given inputs first (uniform branches kept out of the draw code)
         static_for<0, nq>([&](auto q) {
             const uint64_t i = (w0 + wb + q()) * 64 + lane;
             valid[q()] = i < batch;
             fm[q()] = 0;
             oc[q()] = 0;
-            if (valid[q()]) {
-                if (gs.faulty_mode == 0) fm[q()] = faulty[i];
-                if (gs.order_mode == 0) oc[q()] = order[i];
-                if constexpr (PK > 0) gen_trial_u<N, PK>(seed, gs, first_trial + i, fm[q()], oc[q()]);
-                else gen_trial(N, seed, gs, first_trial + i, fm[q()], oc[q()]);
+        });
+        if (gs.faulty_mode == 0)
+            static_for<0, nq>([&](auto q) {
+                if (valid[q()]) fm[q()] = faulty[(w0 + wb + q()) * 64 + lane];
+            });
+        if (gs.order_mode == 0)
+            static_for<0, nq>([&](auto q) {
+                if (valid[q()]) oc[q()] = order[(w0 + wb + q()) * 64 + lane];
+            });
+        static_for<0, nq>([&](auto q) {
+            const uint64_t t = first_trial + (w0 + wb + q()) * 64 + lane;
+            if constexpr (PK > 0) gen_trial_u<N, PK>(seed, gs, t, fm[q()], oc[q()]);
+            else if constexpr (PK == 0) {
+                if (valid[q()]) gen_trial(N, seed, gs, t, fm[q()], oc[q()]);
             }
         });
         static_for<0, nq>([&](auto q) {
@@ -683,7 +693,14 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
         {
             const uint32_t pk = gs.faulty_mode == 0 ? 0u : (gs.f < (uint32_t)N ? gs.f : (uint32_t)N);
             uint64_t* in0 = img + G::oIN;
-            if (pk <= 2) gen_words<N, W, 2>(in0, lane, w0, seed, gs, first_trial, batch, faulty, order);
+            if (gs.faulty_mode == 0 && gs.order_mode == 0) {  // staged inputs: loads only
+                gen_words<N, W, -1>(in0, lane, w0, seed, gs, first_trial, batch, faulty, order);
+            } else if constexpr ((DIAG & 16) != 0) {  // lab: near-free stand-in inputs
+                static_for<0, W>([&](auto wq) {
+                    const uint64_t h = (w0 + wq() + 1) * 0x9E3779B97F4A7C15ull;
+                    if (lane < (uint32_t)NIN) in0[wq() * NIN + lane] = lane == N + 2 ? ~0ull : (h >> lane) & (h << 3);
+                });
+            } else if (pk <= 2) gen_words<N, W, 2>(in0, lane, w0, seed, gs, first_trial, batch, faulty, order);
             else if (pk <= 3) gen_words<N, W, 3>(in0, lane, w0, seed, gs, first_trial, batch, faulty, order);
             else if (pk <= 6) gen_words<N, W, 6>(in0, lane, w0, seed, gs, first_trial, batch, faulty, order);
             else gen_words<N, W, 0>(in0, lane, w0, seed, gs, first_trial, batch, faulty, order);
@@ -799,6 +816,14 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
         FUSED_STAMP(3);
         // ---- per-trial epilogue: lane = trial, all W words unrolled (branch-free
         //      except the stores, so the words' LDS reads and logic interleave) --
+        if constexpr ((DIAG & 32) != 0) {  // lab: near-free stand-in epilogue
+            static_for<0, W>([&](auto wq) {
+                const uint64_t i = (w0 + wq()) * 64 + lane;
+                if (i < batch) decisions[i] = img[G::oAU + wq() * 2 * L + (lane & 15)];
+            });
+        } else {
+        uint64_t dec_out[W];
+        uint32_t out_out[W];
         static_for<0, W>([&](auto wq) {
             constexpr int w = wq();
             const uint64_t* inw = img + G::oIN + w * NIN;
@@ -829,11 +854,19 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
             tc.v[C_VIOL] += lv & inb & ((agree ^ 1u) | (appl & (valid ^ 1u)));
             tc.v[C_FTOT] += lv * r.nf;
             tc.v[C_ATT] += lv * r.nA;
-            if (live) {
-                if (!(DIAG & 1) && decisions) decisions[i] = r.dec;
-                if (!(DIAG & 2) && outcome) outcome[i] = (uint8_t)r.out;
+            dec_out[w] = r.dec;
+            out_out[w] = live ? r.out : 0xFFu;  // 0xFF: not a trial of this batch
+            (void)i;
+        });
+        // stores after all the words' logic (one basic block above)
+        static_for<0, W>([&](auto wq) {
+            const uint64_t i = (w0 + wq()) * 64 + lane;
+            if (out_out[wq()] != 0xFFu) {
+                if (!(DIAG & 1) && decisions) decisions[i] = dec_out[wq()];
+                if (!(DIAG & 2) && outcome) outcome[i] = (uint8_t)out_out[wq()];
             }
         });
+        }
         __builtin_amdgcn_wave_barrier();
         FUSED_STAMP(4);
     }
@@ -846,7 +879,15 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
         for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
         if (lane == (uint32_t)c) mine = x;
     }
-    if (!(DIAG & 4)) sink_counters(lane, mine, blockIdx.x * wpb + wv, gridDim.x * wpb, counters, sk);
+    // the block's waves combine in LDS, then one sink unit per block
+    __shared__ unsigned long long wcnt[kWaveThreads / 64][16];
+    if (lane < 16) wcnt[wv][lane] = mine;
+    __syncthreads();
+    if (wv == 0 && !(DIAG & 4)) {
+        uint64_t tot = 0;
+        for (uint32_t k = 0; k < wpb; ++k) tot += lane < 16 ? wcnt[k][lane] : 0;
+        sink_counters(lane, tot, blockIdx.x, gridDim.x, counters, sk);
+    }
 #ifdef BA_FUSED_STAMPS
     if (lane == 0 && blockIdx.x * wpb + wv < (uint32_t)kPartialRows)
     {

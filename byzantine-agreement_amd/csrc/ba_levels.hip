@@ -283,6 +283,32 @@ hipError_t launch_reduce(const uint64_t* partials, int rows, uint64_t* counters,
     return hipGetLastError();
 }
 
+// Synthetic per-trial inputs to HBM (ba_gen_inputs_device): one thread per
+// trial, the draws of gen_trial, so a GIVEN-mode run on them equals the run
+// that draws them itself.
+__global__ __launch_bounds__(kBlock) void k_gen_inputs(uint32_t n, uint64_t seed, GenSpec gs,
+                                                        uint64_t first_trial, uint64_t batch,
+                                                        uint32_t* __restrict__ faulty_out,
+                                                        uint8_t* __restrict__ order_out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < batch;
+         i += (uint64_t)gridDim.x * kBlock) {
+        uint32_t fm = 0, oc = 0;
+        gen_trial(n, seed, gs, first_trial + i, fm, oc);
+        if (faulty_out) faulty_out[i] = fm;
+        if (order_out) order_out[i] = (uint8_t)oc;
+    }
+}
+
+hipError_t launch_gen_inputs(const RunArgs& a, uint32_t* faulty_out, uint8_t* order_out) {
+    uint64_t blocks = (a.batch + kBlock - 1) / kBlock;
+    if (blocks > 8ull * a.cu_count) blocks = 8ull * a.cu_count;
+    if (blocks < 1) blocks = 1;
+    ProfScope ps(a.prof, "k_gen_inputs", a.stream);
+    hipLaunchKernelGGL(k_gen_inputs, dim3((uint32_t)blocks), dim3(kBlock), 0, a.stream, a.n, a.seed,
+                       a.gen, a.first_trial, a.batch, faulty_out, order_out);
+    return hipGetLastError();
+}
+
 hipError_t launch_table(const RunArgs& a, uint64_t* partials) {
     const uint32_t blocks = blocks_for(a.batch, kPartialRows);
     ProfScope ps(a.prof, "k_table", a.stream);

@@ -163,6 +163,19 @@ int ba_run_trials_device(struct ba_ctx* ctx, const ba_params* p, uint64_t batch,
                          uint64_t* d_decisions, uint8_t* d_outcome, uint64_t* d_counters,
                          void* stream);
 
+/* Synthetic inputs of trials [p->first_trial, p->first_trial + batch): the
+ * faulty sets (p->faulty_mode RANDOM or EXACT) and commander orders
+ * (p->order_mode RANDOM or CONST) that ba_run_trials_device would otherwise
+ * draw itself -- the same Philox stream, so running the batch on these as
+ * BA_FAULTY_GIVEN / BA_ORDER_GIVEN inputs gives bit-identical results.  This
+ * stages a workload's per-trial inputs in HBM ahead of time (bench.py does so
+ * before its timed region; the lies stay inside the run: they are the faulty
+ * generals' coin flips during the protocol, ba.py:45, 269).  Either output may
+ * be NULL; a non-NULL one whose mode is GIVEN is BA_EINVAL.  Asynchronous on
+ * `stream` (NULL = HIP's null stream). */
+int ba_gen_inputs_device(struct ba_ctx* ctx, const ba_params* p, uint64_t batch,
+                         uint32_t* d_faulty_mask, uint8_t* d_order, void* stream);
+
 /* ---- one huge instance split by first-hop subtree --------
  * The subtree of first-hop lieutenant j (relay paths starting 0 -> j) needs
  * only L_0[j]; its relay levels and inner majorities are independent of the

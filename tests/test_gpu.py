@@ -319,3 +319,39 @@ def test_om3_wave_block_generic_vs_oracle(monkeypatch, n, m, f, fmode):
         same(res.decisions, od, "decisions " + tag)
         same(res.outcome, oo, "outcome " + tag)
         assert {k: res.counters[k] for k in ocnt} == ocnt, tag
+
+
+@pytest.mark.parametrize("n,m,fmode,f,omode", [(10, 3, 1, 3, 1), (10, 3, 2, 4, 2), (13, 4, 1, 4, 1),
+                                               (4, 1, 2, 1, 1), (16, 2, 1, 5, 1), (7, 3, 1, 7, 2)])
+def test_staged_inputs_equal_in_kernel_draws(engine, n, m, fmode, f, omode):
+    """ba_gen_inputs_device + GIVEN-mode run == the run that draws its own
+    inputs (bench.py stages inputs this way), on every engine; the staged
+    inputs themselves equal the oracle's generator."""
+    import ctypes
+    import torch
+    from ba_amd import lib as L
+    B, first = 64 * 41 + 9, 64 * 123
+    kw = dict(seed=0x5EED + n, faulty_mode=fmode, f=f, order_mode=omode, order_value=1,
+              first_trial=first)
+    fm = torch.zeros(B, dtype=torch.int32, device="cuda")
+    oc = torch.zeros(B, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    p = L.make_params(n, m, kw["seed"], L.LIE_PHILOX, fmode, f, omode, 1, L.ENGINE_AUTO, first)
+    engine.gen_inputs_device(p, B, d_faulty=fm.data_ptr(), d_order=oc.data_ptr(), stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    fm_h = fm.cpu().numpy().view(np.uint32)
+    oc_h = oc.cpu().numpy()
+    lib = oracle_c.load()
+    for t in (0, 1, 63, 64, B - 1):
+        a, b = ctypes.c_uint32(), ctypes.c_uint8()
+        lib.ba_oracle_gen(n, kw["seed"], fmode, f, omode, 1, first + t, ctypes.byref(a), ctypes.byref(b))
+        assert (int(fm_h[t]), int(oc_h[t])) == (a.value, b.value), t
+    for eng in _engines(n, m):
+        drawn = engine.run(n, m, B, engine=eng, **kw)
+        given = engine.run(n, m, B, seed=kw["seed"], faulty=fm_h, order=oc_h, first_trial=first,
+                           engine=eng)
+        same(given.decisions, drawn.decisions, f"decisions engine={eng}")
+        same(given.outcome, drawn.outcome, f"outcome engine={eng}")
+        assert given.counters == drawn.counters
+    with pytest.raises(L.BAError):
+        engine.gen_inputs_device(L.make_params(n, m, 1), B, d_faulty=fm.data_ptr())

@@ -372,7 +372,14 @@ static int compare_wave(uint64_t B) {
     printf("{\"wave_lds56k_us\": %.2f}\n", vpad);
     const float vprio = time_launch(k_om3w<10, 8>, gridw, ldsw, 0xBA5EEDull, gs, 0ull, B,
                                   (const uint32_t*)nullptr, (const uint8_t*)nullptr, d2, o2, c2, g_sink);
-    printf("{\"wave_prio_alt_us\": %.2f}\n", vprio);
+    printf("{\"wave_prio_off_us\": %.2f}\n", vprio);
+    const float vng = time_launch(k_om3w<10, 16>, gridw, ldsw, 0xBA5EEDull, gs, 0ull, B,
+                                  (const uint32_t*)nullptr, (const uint8_t*)nullptr, d2, o2, c2, g_sink);
+    const float vne = time_launch(k_om3w<10, 32>, gridw, ldsw, 0xBA5EEDull, gs, 0ull, B,
+                                  (const uint32_t*)nullptr, (const uint8_t*)nullptr, d2, o2, c2, g_sink);
+    const float vnn = time_launch(k_om3w<10, 48>, gridw, ldsw, 0xBA5EEDull, gs, 0ull, B,
+                                  (const uint32_t*)nullptr, (const uint8_t*)nullptr, d2, o2, c2, g_sink);
+    printf("{\"wave_no_gen_us\": %.2f, \"wave_no_epi_us\": %.2f, \"wave_no_gen_no_epi_us\": %.2f}\n", vng, vne, vnn);
     printf("{\"wave_no_dec_us\": %.2f, \"wave_no_out_us\": %.2f, \"wave_no_atomic_us\": %.2f, \"wave_none_us\": %.2f}\n",
            v1, v2, v4, v7);
     return bad || badc;
