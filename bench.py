@@ -35,6 +35,18 @@ sys.path.insert(0, os.path.join(ROOT, "byzantine-agreement_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# Philox4x32-10 issue ceiling of one MI355X (tools/philox_bench.hip, best code
+# shape: v_mad_u64_u32 + v_bitop3 xor3, 8 waves/SIMD; profiles/r01_philox_bench.jsonl)
+PHILOX_PEAK_CALLS = 9.69e11
+
+
+def philox_calls_per_trial_word(n: int, m: int) -> int:
+    """Fewest Philox4x32-10 calls that produce every lie bit of a 64-trial word:
+    each call yields two slot-words, so level k needs ceil(|L_k| / 2) calls."""
+    from ba_amd import lib as L
+    lib = L.load()
+    me = L.effective_depth(n, m)
+    return sum((lib.ba_level_slots(n, m, k) + 1) // 2 for k in range(me + 1))
 
 
 def cpu_model() -> str:
@@ -228,7 +240,7 @@ def main():
         value_gen = total_trials / T2
 
     # per-kernel HIP-event timing on the launch stream (a second pass of the same steps)
-    kernels, roof = {}, None
+    kernels, roof, compute_roof = {}, None, None
     if not args.no_profile:
         eng.profile(True)
         for i in range(args.steps):
@@ -248,7 +260,19 @@ def main():
                     "traffic": round(traffic) if traffic else None,
                     "algorithmic_bytes_per_launch": alg,
                     "traffic_source": src,
-                    "valu_util": round(valu, 4) if valu else None}
+                    "valu_util": round(valu, 4) if valu else None,
+                    "note": "algorithmic bytes = SURVEY.md 8d's level-synchronous figure; the "
+                            "fused kernel keeps the tree in LDS/registers, so frac > 1 means it "
+                            "beats that design, and compute_roofline is its real bound"}
+            words = (B + 63) // 64
+            calls = philox_calls_per_trial_word(n, m) * words
+            rate = calls / (avg_ms * 1e-3)
+            compute_roof = {"bound": "valu (Philox4x32-10 lie draws)", "kernel": name,
+                            "achieved": round(rate / 1e9, 2), "peak": round(PHILOX_PEAK_CALLS / 1e9, 2),
+                            "unit": "G Philox calls/s", "frac": round(rate / PHILOX_PEAK_CALLS, 4),
+                            "calls_per_launch": calls,
+                            "floor_ms": round(calls / PHILOX_PEAK_CALLS * 1e3, 4),
+                            "peak_source": "profiles/r01_philox_bench.jsonl"}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = run_cpu_baseline(n, m, args.seed, fmax, args.cpu_budget_s)
@@ -259,7 +283,7 @@ def main():
             "value": round(value, 1), "unit": "trial-decisions/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(T * 1e3 / args.steps, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
-            "data": "synthetic (Philox-generated faulty sets, orders and lies on device)",
+            "data": "synthetic (Philox-generated faulty sets and orders staged in HBM, lies drawn in-kernel)",
             "config": {"workload": f"OM({m}) n={n}, {B} trials/GPU/step, f~U{{0..{fmax}}}, "
                                    f"random order, decisions+outcome written",
                        "n": n, "m": m, "trials_per_gpu_step": B, "engine": args.engine,
@@ -270,6 +294,7 @@ def main():
             "gpu_event_ms": round(gpu_ms, 3),
             "kernels_ms": {k: round(v[1] / v[0], 4) for k, v in kernels.items()},
             "roofline": roof,
+            "compute_roofline": compute_roof,
             "cpu_baseline": cpu,
             "counters": counters,
         }

@@ -66,6 +66,34 @@ __host__ __device__ __forceinline__ P4 philox10(P4 c, uint32_t k0, uint32_t k1) 
     return c;
 }
 
+// G independent Philox4x32-10 calls advanced round by round in lockstep: the
+// source order interleaves the chains, so each v_mad_u64_u32 result is used G
+// instructions later instead of right away (left to itself the scheduler runs
+// the calls one after another and exposes the multiply latency).
+template <int G>
+__host__ __device__ __forceinline__ void philox10_n(P4 (&c)[G], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        uint64_t p0[G], p1[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            p0[g] = (uint64_t)0xD2511F53u * c[g].x;
+            p1[g] = (uint64_t)0xCD9E8D57u * c[g].z;
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            P4 n;
+            n.x = xor3_32((uint32_t)(p1[g] >> 32), c[g].y, k0);
+            n.y = (uint32_t)p1[g];
+            n.z = xor3_32((uint32_t)(p0[g] >> 32), c[g].w, k1);
+            n.w = (uint32_t)p0[g];
+            c[g] = n;
+        }
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
 // Lie words of slots 2*pair and 2*pair+1 at level k for global trial word gw.
 __device__ __forceinline__ void lie_pair(uint64_t seed, uint32_t k, uint32_t pair, uint64_t gw,
                                          uint64_t& lie0, uint64_t& lie1) {
@@ -73,6 +101,22 @@ __device__ __forceinline__ void lie_pair(uint64_t seed, uint32_t k, uint32_t pai
                     (uint32_t)(seed >> 32));
     lie0 = (uint64_t)o.y << 32 | o.x;
     lie1 = (uint64_t)o.w << 32 | o.z;
+}
+
+// G consecutive slot pairs pair0 .. pair0+G-1 of level k, word gw, interleaved;
+// lie[2q], lie[2q+1] = the two slot-words of pair pair0+q.
+template <int G>
+__device__ __forceinline__ void lie_pairs(uint64_t seed, uint32_t k, uint32_t pair0, uint64_t gw,
+                                          uint64_t (&lie)[2 * G]) {
+    P4 c[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) c[g] = P4{pair0 + (uint32_t)g, k, (uint32_t)gw, (uint32_t)(gw >> 32)};
+    philox10_n<G>(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        lie[2 * g] = (uint64_t)c[g].y << 32 | c[g].x;
+        lie[2 * g + 1] = (uint64_t)c[g].w << 32 | c[g].z;
+    }
 }
 
 __device__ __forceinline__ uint32_t mulhi_range(uint32_t u, uint32_t range) {

@@ -36,20 +36,26 @@ __device__ __forceinline__ void static_for(F&& f) {
 // direct value, also every loyal row's broadcast), Fm[a] = faulty word of j_a.
 // Column b counts diag[b] then rows a != b in row order, so the carry-save
 // counters see a compile-time input schedule (Csa, ba_device.hpp).
+// The S(S-1)/2 Philox calls run in interleaved groups of PG (philox10_n);
+// each group's 2*PG lie words feed the counters before the next group starts.
+constexpr int leaf_philox_group(int npair) { return npair % 3 == 0 ? 3 : (npair % 4 == 0 ? 4 : (npair % 2 == 0 ? 2 : 3)); }
+
 template <int S>
 __device__ __forceinline__ void leaf_block(uint32_t me, uint64_t seed, uint64_t gw, uint32_t sr,
                                            const uint64_t (&diag)[S], const uint64_t (&Fm)[S],
                                            uint64_t (&R)[S]) {
     constexpr int NL = planes_c(S);
     constexpr int NPAIR = S * (S - 1) / 2;
+    constexpr int PG = leaf_philox_group(NPAIR);
     Csa<NL> cnt[S];
     static_for<0, S>([&](auto b) { cnt[b()].template add<0>(diag[b()]); });
     const uint32_t pair0 = sr * (uint32_t)NPAIR;  // leaf block base slot sr*S*(S-1) is even
-    static_for<0, NPAIR>([&](auto q) {
-        uint64_t lw[2];
-        lie_pair(seed, me, pair0 + q(), gw, lw[0], lw[1]);
-        static_for<0, 2>([&](auto h) {
-            constexpr int e = 2 * q() + h();     // slot within the block: row a, column c
+    static_for<0, (NPAIR + PG - 1) / PG>([&](auto grp) {
+        constexpr int q0 = grp() * PG, ng = NPAIR - q0 < PG ? NPAIR - q0 : PG;
+        uint64_t lw[2 * ng];
+        lie_pairs<ng>(seed, me, pair0 + q0, gw, lw);
+        static_for<0, 2 * ng>([&](auto h) {
+            constexpr int e = 2 * q0 + h();      // slot within the block: row a, column c
             constexpr int a = e / (S - 1);
             constexpr int c = e % (S - 1);
             constexpr int b = c + (c >= a);      // receiver's rank among the S members
@@ -746,21 +752,28 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
             const uint32_t j2 = la + (la >= j1);
             uint64_t par = 0;
             if (act) {
-                // 1. L1[j1, a]: sender j1 relays L0[j1]
-                uint64_t l1[2];
-                lie_pair(seed, 1, sr >> 1, gw, l1[0], l1[1]);
-                const uint64_t lie = (sr & 1u) ? l1[1] : l1[0];
+                // 1. L1[j1, a] (sender j1 relays L0[j1]) and the level-2 diagonal
+                //    pairs of leaf block (j1, a): one interleaved Philox group
+                const uint32_t x0 = sr * S;
+                constexpr int NPD = (S + 1) / 2;
+                P4 pc[NPD + 1];
+                static_for<0, NPD>([&](auto qd) {
+                    pc[qd()] = P4{(x0 >> 1) + qd(), 2u, (uint32_t)gw, (uint32_t)(gw >> 32)};
+                });
+                pc[NPD] = P4{sr >> 1, 1u, (uint32_t)gw, (uint32_t)(gw >> 32)};
+                philox10_n<NPD + 1>(pc, (uint32_t)seed, (uint32_t)(seed >> 32));
+                uint64_t lw2[2 * NPD];
+                static_for<0, NPD>([&](auto qd) {
+                    lw2[2 * qd()] = (uint64_t)pc[qd()].y << 32 | pc[qd()].x;
+                    lw2[2 * qd() + 1] = (uint64_t)pc[qd()].w << 32 | pc[qd()].z;
+                });
+                const uint64_t lie = (sr & 1u) ? ((uint64_t)pc[NPD].w << 32 | pc[NPD].z)
+                                               : ((uint64_t)pc[NPD].y << 32 | pc[NPD].x);
                 const uint64_t fj = in[j1 + 1];
                 par = (fj & lie) | (~fj & img[G::oL0 + lw * L + j1]);
                 // 2. leaf block (j1, a): level-2 diagonal, then S(S-1) leaves
                 const uint32_t lo = j1 < j2 ? j1 : j2, hi = j1 < j2 ? j2 : j1;
                 const uint64_t fs = in[j2 + 1];  // level-2 sender: j2
-                const uint32_t x0 = sr * S;
-                constexpr int NPD = (S + 1) / 2;
-                uint64_t lw2[2 * NPD];
-                static_for<0, NPD>([&](auto qd) {
-                    lie_pair(seed, 2, (x0 >> 1) + qd(), gw, lw2[2 * qd()], lw2[2 * qd() + 1]);
-                });
                 const uint64_t oddmask = 0ull - (uint64_t)(x0 & 1u);
                 uint64_t diag[S], Fm[S], R[S];
                 static_for<0, S>([&](auto a) {

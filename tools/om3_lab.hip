@@ -6,6 +6,7 @@
 //   run:   tools/om3_lab [batch]
 #define BA_FUSED_STAMPS 1
 #include "../byzantine-agreement_amd/csrc/ba_fused.hip"
+#include "../byzantine-agreement_amd/csrc/ba_levels.hip"
 
 #include <cstdio>
 #include <cstdlib>
@@ -373,6 +374,51 @@ static int compare_wave(uint64_t B) {
     const float vprio = time_launch(k_om3w<10, 8>, gridw, ldsw, 0xBA5EEDull, gs, 0ull, B,
                                   (const uint32_t*)nullptr, (const uint8_t*)nullptr, d2, o2, c2, g_sink);
     printf("{\"wave_prio_off_us\": %.2f}\n", vprio);
+    {
+        uint32_t* sf;
+        uint8_t* so;
+        (void)hipMalloc(&sf, B * 4);
+        (void)hipMalloc(&so, B);
+        hipLaunchKernelGGL(k_gen_inputs, dim3(2048), dim3(256), 0, 0, 10u, 0xBA5EEDull, gs, 0ull, B, sf, so);
+        GenSpec gg{0, 3, 0, 1};
+        const float vst = time_launch(k_om3w<10>, gridw, ldsw, 0xBA5EEDull, gg, 0ull, B,
+                                      (const uint32_t*)sf, (const uint8_t*)so, d2, o2, c2, g_sink);
+        const float vst2 = time_launch(k_om3w<10, 32>, gridw, ldsw, 0xBA5EEDull, gg, 0ull, B,
+                                       (const uint32_t*)sf, (const uint8_t*)so, d2, o2, c2, g_sink);
+        printf("{\"wave_staged_us\": %.2f, \"wave_staged_no_epi_us\": %.2f}\n", vst, vst2);
+        // cold staged inputs: rotate over 64 batches (> the 256 MB Infinity Cache)
+        const int NB = 64;
+        uint32_t* cf;
+        uint8_t* co;
+        (void)hipMalloc(&cf, B * 4 * NB);
+        (void)hipMalloc(&co, B * NB);
+        for (int k = 0; k < NB; ++k)
+            hipLaunchKernelGGL(k_gen_inputs, dim3(2048), dim3(256), 0, 0, 10u, 0xBA5EEDull, gs,
+                               (uint64_t)k * B, B, cf + k * B, co + k * B);
+        (void)hipDeviceSynchronize();
+        hipEvent_t e0, e1;
+        (void)hipEventCreate(&e0);
+        (void)hipEventCreate(&e1);
+        (void)hipEventRecord(e0, 0);
+        for (int k = 0; k < NB; ++k)
+            hipLaunchKernelGGL(k_om3w<10>, dim3(gridw), dim3(256), ldsw, 0, 0xBA5EEDull, gg,
+                               (uint64_t)k * B, B, (const uint32_t*)(cf + k * B),
+                               (const uint8_t*)(co + k * B), d2, o2, c2, g_sink);
+        (void)hipEventRecord(e1, 0);
+        (void)hipEventSynchronize(e1);
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        (void)hipEventRecord(e0, 0);
+        for (int k = 0; k < NB; ++k)
+            hipLaunchKernelGGL(k_om3w<10>, dim3(gridw), dim3(256), ldsw, 0, 0xBA5EEDull, gs,
+                               (uint64_t)k * B, B, (const uint32_t*)nullptr, (const uint8_t*)nullptr,
+                               d2, o2, c2, g_sink);
+        (void)hipEventRecord(e1, 0);
+        (void)hipEventSynchronize(e1);
+        float ms2 = 0;
+        (void)hipEventElapsedTime(&ms2, e0, e1);
+        printf("{\"wave_staged_cold_us\": %.2f, \"wave_inkernel_same_seq_us\": %.2f}\n", ms * 1000 / NB, ms2 * 1000 / NB);
+    }
     const float vng = time_launch(k_om3w<10, 16>, gridw, ldsw, 0xBA5EEDull, gs, 0ull, B,
                                   (const uint32_t*)nullptr, (const uint8_t*)nullptr, d2, o2, c2, g_sink);
     const float vne = time_launch(k_om3w<10, 32>, gridw, ldsw, 0xBA5EEDull, gs, 0ull, B,
