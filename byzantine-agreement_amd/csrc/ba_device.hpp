@@ -318,10 +318,13 @@ __device__ __forceinline__ TrialResult trial_result(uint32_t n, uint32_t me, uin
     const uint32_t loyal = lts & ~fm;
     const uint32_t la = A & loyal, lu = U & loyal, lr = loyal & ~A & ~U;
     const uint32_t agree = ((la != 0) + (lu != 0) + (lr != 0)) <= 1;
-    const uint32_t appl = (fm & 1u) == 0;
-    const uint32_t valid = appl && (oc == 1 ? la == loyal : lr == loyal);
+    // bitwise & and selects only: a short-circuit && here became divergent
+    // branches that split the WAVE epilogue into one basic block per word
+    const uint32_t appl = (fm & 1u) == 0 ? 1u : 0u;
+    const uint32_t okA = la == loyal ? 1u : 0u, okR = lr == loyal ? 1u : 0u;
+    const uint32_t valid = appl & (oc == 1 ? okA : okR);
     const uint32_t nf = __popc(fm);
-    const uint32_t inb = nf <= me && n > 3 * me;
+    const uint32_t inb = (nf <= me ? 1u : 0u) & (n > 3 * me ? 1u : 0u);
     TrialResult r;
     r.dec = part1by1(A >> 1) | (part1by1(U >> 1) << 1);
     r.out = q | agree << 2 | appl << 3 | valid << 4 | inb << 5;

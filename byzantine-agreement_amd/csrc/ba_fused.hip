@@ -547,10 +547,13 @@ __global__ __launch_bounds__(kFusedThreads, ((N - 3) <= 7 ? 4 : 2)) void k_fused
 //   3. lane (w, b = a): R1[j1, b] = maj(L1[j1, b], R2[j1, a', b] : a' != b),
 //      added into the bit-sliced root counter of receiver column j2(b)
 // R1 is never stored: each root column accumulates as the subtrees finish.
+// R2 is stored receiver-major (R2T[w][b][a] = R2[j1, a, b], with the lane's
+// own L1[j1, b] on the diagonal a == b), so step 3 counts C contiguous words
+// with a compile-time carry-save schedule.
 // Lie bits are keyed exactly as in k_fused3 (level, global slot pair, global
 // word), so both kernels give identical results.
 // LDS per wave (uint64 words): IN[W][N+3] (F[N] OB OO VAL) | L0[W][L] |
-// R2[W][C][S] | RC[W][L][P] (root counters) ; A/U roots reuse R2 when it fits.
+// R2T[W][C][C] | RC[W][L][P] (root counters) ; A/U roots reuse R2T when it fits.
 // ---------------------------------------------------------------------------
 // Branch-free synthetic inputs for compile-time N: the same draws as
 // gen_trial (ba_device.hpp), but every Philox call is issued up front, the
@@ -660,9 +663,9 @@ struct Om3W {
     static constexpr int LANES = W * C;            // lanes busy in the subtree rounds
     static constexpr int P = planes_c(L);          // root counter planes (L inputs)
     static constexpr int NIN = N + 3;
-    static constexpr int oIN = 0, oL0 = oIN + W * NIN, oR2 = oL0 + W * L, oRC = oR2 + W * C * S;
+    static constexpr int oIN = 0, oL0 = oIN + W * NIN, oR2 = oL0 + W * L, oRC = oR2 + W * C * C;
     static constexpr int end0 = oRC + W * L * P;
-    static constexpr bool au_in_r2 = 2 * L <= C * S;
+    static constexpr bool au_in_r2 = 2 * L <= C * C;
     static constexpr int oAU = au_in_r2 ? oR2 : end0;
     static constexpr int words = ((au_in_r2 ? end0 : end0 + W * 2 * L) + 1) & ~1;
 };
@@ -785,23 +788,20 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
                     Fm[a()] = in[ida + 1];
                 });
                 leaf_block<S>(ME, seed, gw, sr, diag, Fm, R);
-                uint64_t* r2 = img + G::oR2 + (lw * C + la) * S;
-                static_for<0, S>([&](auto d) { r2[d()] = R[d()]; });
+                // receiver-major: member d of block a is receiver b = d + (d >= a)
+                uint64_t* r2t = img + G::oR2 + lw * C * C + la;
+                r2t[la * C] = par;
+                static_for<0, S>([&](auto d) { r2t[(d() + (d() >= la ? 1u : 0u)) * C] = R[d()]; });
             }
             __builtin_amdgcn_wave_barrier();
             FUSED_STAMP(1);
             if (act) {
                 // 3. R1[j1, b], b = la: L1[j1, b] (this lane's own parent) plus
                 //    column b of the word's other leaf blocks a' != b
-                const uint32_t b = la;
-                Count<planes_c(C)> cnt;
-                cnt.add(par);
-                const uint64_t* r2w = img + G::oR2 + lw * C * S;
-                static_for<0, C>([&](auto a) {
-                    if (a() == b) return;
-                    cnt.add(r2w[a() * S + (a() < b ? b - 1 : b)]);
-                });
-                const uint64_t r1 = cnt.ge(C / 2 + 1);  // inner tie -> non-attack
+                const uint64_t* col = img + G::oR2 + (lw * C + la) * C;
+                Csa<planes_c(C)> cnt;
+                static_for<0, C>([&](auto a) { cnt.template add<a()>(col[a()]); });
+                const uint64_t r1 = cnt.template ge<C, C / 2 + 1>();  // inner tie -> non-attack
                 // root column j2 += R1[j1, b] (ripple add on the bit-sliced planes)
                 uint64_t* rc = img + G::oRC + (lw * L + j2) * P;
                 uint64_t x = r1;
@@ -835,50 +835,56 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
                 if (i < batch) decisions[i] = img[G::oAU + wq() * 2 * L + (lane & 15)];
             });
         } else {
-        uint64_t dec_out[W];
-        uint32_t out_out[W];
-        static_for<0, W>([&](auto wq) {
-            constexpr int w = wq();
-            const uint64_t* inw = img + G::oIN + w * NIN;
-            const uint64_t* au = img + G::oAU + w * 2 * L;
-            const uint64_t i = (w0 + w) * 64 + lane;
-            const bool live = (inw[N + 2] >> lane) & 1ull;
-            uint32_t A = 0, U = 0, fm = 0;
-            static_for<0, L>([&](auto b) {
-                A |= (uint32_t)((au[b()] >> lane) & 1ull) << (b() + 1);
-                U |= (uint32_t)((au[L + b()] >> lane) & 1ull) << (b() + 1);
+        // two words per iteration: their LDS reads and logic interleave without
+        // the register blow-up (and spills) of unrolling all W words at once
+        constexpr int EW = 2;
+#pragma unroll 1
+        for (int wb = 0; wb < W; wb += EW) {
+            uint64_t dec_out[EW];
+            uint32_t out_out[EW];
+            static_for<0, EW>([&](auto wq) {
+                const int w = wb + wq();
+                out_out[wq()] = 0xFFu;  // 0xFF: not a trial of this batch
+                dec_out[wq()] = 0;
+                if (W % EW != 0 && w >= W) return;
+                const uint64_t* inw = img + G::oIN + w * NIN;
+                const uint64_t* au = img + G::oAU + w * 2 * L;
+                const bool live = (inw[N + 2] >> lane) & 1ull;
+                uint32_t A = 0, U = 0, fm = 0;
+                static_for<0, L>([&](auto b) {
+                    A |= (uint32_t)((au[b()] >> lane) & 1ull) << (b() + 1);
+                    U |= (uint32_t)((au[L + b()] >> lane) & 1ull) << (b() + 1);
+                });
+                static_for<0, N>([&](auto g) { fm |= (uint32_t)((inw[g()] >> lane) & 1ull) << g(); });
+                const uint32_t ob = (uint32_t)(inw[N] >> lane) & 1u;
+                const uint32_t oo = (uint32_t)(inw[N + 1] >> lane) & 1u;
+                const TrialResult r = trial_result(N, ME, fm, oo ? 2u : ob, A, U);
+                const uint32_t lv = live ? 1u : 0u;
+                const uint32_t q = r.out & 3, agree = (r.out >> 2) & 1, appl = (r.out >> 3) & 1;
+                const uint32_t valid = (r.out >> 4) & 1, inb = (r.out >> 5) & 1;
+                tc.v[C_TRIALS] += lv;
+                tc.v[C_AGREE] += lv & agree;
+                tc.v[C_VAPPL] += lv & appl;
+                tc.v[C_VALID] += lv & valid;
+                tc.v[C_QR] += lv & (q == 0);
+                tc.v[C_QA] += lv & (q == 1);
+                tc.v[C_QU] += lv & (q == 2);
+                tc.v[C_UNDEF] += lv * r.nU;
+                tc.v[C_INB] += lv & inb;
+                tc.v[C_VIOL] += lv & inb & ((agree ^ 1u) | (appl & (valid ^ 1u)));
+                tc.v[C_FTOT] += lv * r.nf;
+                tc.v[C_ATT] += lv * r.nA;
+                dec_out[wq()] = r.dec;
+                out_out[wq()] = live ? r.out : 0xFFu;
             });
-            static_for<0, N>([&](auto g) { fm |= (uint32_t)((inw[g()] >> lane) & 1ull) << g(); });
-            const uint32_t ob = (uint32_t)(inw[N] >> lane) & 1u;
-            const uint32_t oo = (uint32_t)(inw[N + 1] >> lane) & 1u;
-            const TrialResult r = trial_result(N, ME, fm, oo ? 2u : ob, A, U);
-            const uint32_t lv = live ? 1u : 0u;
-            const uint32_t q = r.out & 3, agree = (r.out >> 2) & 1, appl = (r.out >> 3) & 1;
-            const uint32_t valid = (r.out >> 4) & 1, inb = (r.out >> 5) & 1;
-            tc.v[C_TRIALS] += lv;
-            tc.v[C_AGREE] += lv & agree;
-            tc.v[C_VAPPL] += lv & appl;
-            tc.v[C_VALID] += lv & valid;
-            tc.v[C_QR] += lv & (q == 0);
-            tc.v[C_QA] += lv & (q == 1);
-            tc.v[C_QU] += lv & (q == 2);
-            tc.v[C_UNDEF] += lv * r.nU;
-            tc.v[C_INB] += lv & inb;
-            tc.v[C_VIOL] += lv & inb & ((agree ^ 1u) | (appl & (valid ^ 1u)));
-            tc.v[C_FTOT] += lv * r.nf;
-            tc.v[C_ATT] += lv * r.nA;
-            dec_out[w] = r.dec;
-            out_out[w] = live ? r.out : 0xFFu;  // 0xFF: not a trial of this batch
-            (void)i;
-        });
-        // stores after all the words' logic (one basic block above)
-        static_for<0, W>([&](auto wq) {
-            const uint64_t i = (w0 + wq()) * 64 + lane;
-            if (out_out[wq()] != 0xFFu) {
-                if (!(DIAG & 1) && decisions) decisions[i] = dec_out[wq()];
-                if (!(DIAG & 2) && outcome) outcome[i] = (uint8_t)out_out[wq()];
-            }
-        });
+            static_for<0, EW>([&](auto wq) {
+                const uint64_t i = (w0 + wb + wq()) * 64 + lane;
+                if (out_out[wq()] != 0xFFu) {
+                    if (!(DIAG & 1) && decisions) decisions[i] = dec_out[wq()];
+                    if (!(DIAG & 2) && outcome) outcome[i] = (uint8_t)out_out[wq()];
+                }
+            });
+        }
         }
         __builtin_amdgcn_wave_barrier();
         FUSED_STAMP(4);
