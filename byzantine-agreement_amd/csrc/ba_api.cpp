@@ -189,7 +189,8 @@ struct DevBuf {
 struct GeoEntry {
     Geometry g;
     DevBuf sender;
-    bool fused_ok = false;
+    bool fused_ok = false;  // some FUSED kernel (WAVE or block) runs this tree
+    bool plan_ok = false;   // the generic block kernel's LDS plan fits
     FusedPlan fp{};
     DevBuf fplan;    // device copy of fp (k_fused reads it through a pointer)
     DevBuf members;  // device copy of g.members
@@ -356,7 +357,7 @@ extern "C" int ba_engine_for(uint32_t n, uint32_t m) {
     Geometry g;
     if (!g.build(n, effective_depth(n, m), 1ull << 31)) return BA_ENGINE_LEVELS;
     FusedPlan fp;
-    return plan_fused(g, fp) ? BA_ENGINE_FUSED : BA_ENGINE_LEVELS;
+    return (wave_supported(g) || plan_fused(g, fp)) ? BA_ENGINE_FUSED : BA_ENGINE_LEVELS;
 }
 
 // ---------------------------------------------------------------------------
@@ -419,8 +420,9 @@ static GeoEntry* geometry(ba_ctx* ctx, uint32_t n, uint32_t me, int* rc) {
             return nullptr;
         }
     }
-    ge->fused_ok = plan_fused(ge->g, ge->fp);
-    if (ge->fused_ok) {
+    ge->plan_ok = plan_fused(ge->g, ge->fp);
+    ge->fused_ok = ge->plan_ok || wave_supported(ge->g);
+    if (ge->plan_ok) {
         if ((*rc = ge->fplan.grow(sizeof(FusedPlan))) != BA_OK) return nullptr;
         hipError_t e = hipMemcpy(ge->fplan.p, &ge->fp, sizeof(FusedPlan), hipMemcpyHostToDevice);
         if (e != hipSuccess) {
@@ -527,11 +529,12 @@ extern "C" int ba_run_trials_device(ba_ctx* ctx, const ba_params* p, uint64_t ba
     a.members = (const uint64_t*)ge->members.p;
     const bool fused_ok = ge->fused_ok;
     if (p->engine == BA_ENGINE_FUSED && !fused_ok)
-        return fail(BA_ENOTSUP, "FUSED engine needs 2 <= m_eff <= %d and n - m_eff <= %d with the "
-                    "per-word tree within %llu B of LDS (n=%u, m_eff=%u)", kFusedMaxDepth,
-                    kMaxLeafS, (unsigned long long)kFusedLdsBudget, a.n, a.me);
+        return fail(BA_ENOTSUP, "FUSED engine needs m_eff = 3 (5 <= n <= 14) or 4 (6 <= n <= %u), "
+                    "or 2 <= m_eff <= %d and n - m_eff <= %d with the per-word tree within "
+                    "%llu B of LDS (n=%u, m_eff=%u)", kWave4MaxN, kFusedMaxDepth, kMaxLeafS,
+                    (unsigned long long)kFusedLdsBudget, a.n, a.me);
     if (fused_ok && p->engine != BA_ENGINE_LEVELS) {
-        HIP_TRY(launch_fused(a, g, ge->fp, (const FusedPlan*)ge->fplan.p,
+        HIP_TRY(launch_fused(a, g, ge->plan_ok, ge->fp, (const FusedPlan*)ge->fplan.p,
                              (const uint8_t*)ge->sender.p, partials));
         return BA_OK;
     }

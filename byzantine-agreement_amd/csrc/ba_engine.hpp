@@ -107,6 +107,7 @@ constexpr int kFusedMaxDepth = 6;
 constexpr uint64_t kFusedLdsBudget = 39 * 1024;  // per block: four blocks per CU
 constexpr int kFusedThreads = 256;               // 4 waves: 4 blocks/CU at <= 128 VGPRs
 constexpr int kWaveThreads = 256;                // WAVE engine: 4 independent waves per block
+constexpr uint32_t kWave4MaxN = 14;              // k_om4w instantiated for 6 <= n <= 14
 
 // LDS image of the FUSED engine (one per 64-trial word, WPB words per block).
 struct FusedPlan {
@@ -118,11 +119,12 @@ struct FusedPlan {
 };
 
 bool leaf_supported(const Geometry& g);
+bool wave_supported(const Geometry& g);
 bool plan_fused(const Geometry& g, FusedPlan& fp);
 hipError_t launch_leaf(const Geometry& g, uint64_t seed, uint64_t gw0, uint32_t W,
                        uint32_t srbase, uint32_t srcnt, const uint64_t* Lm1, const uint64_t* F,
                        const uint64_t* d_members, uint64_t* Rm1, hipStream_t st, Prof* prof);
-hipError_t launch_fused(const RunArgs& a, const Geometry& g, const FusedPlan& fp,
+hipError_t launch_fused(const RunArgs& a, const Geometry& g, bool plan_ok, const FusedPlan& fp,
                         const FusedPlan* d_fp, const uint8_t* d_sender, uint64_t* partials);
 
 hipError_t launch_table(const RunArgs& a, uint64_t* partials);

@@ -355,3 +355,44 @@ def test_staged_inputs_equal_in_kernel_draws(engine, n, m, fmode, f, omode):
         assert given.counters == drawn.counters
     with pytest.raises(L.BAError):
         engine.gen_inputs_device(L.make_params(n, m, 1), B, d_faulty=fm.data_ptr())
+
+
+# --- effective depth 4: the WAVE kernel k_om4w vs the oracle -----------------------
+OM4_CASES = [(6, 4, 1), (6, 5, 2), (7, 4, 2), (8, 4, 2), (9, 4, 3), (10, 4, 3), (11, 4, 3),
+             (12, 4, 4), (13, 4, 4), (14, 4, 5)]
+
+
+@pytest.mark.parametrize("n,m,f", OM4_CASES)
+def test_om4_wave_vs_oracle(monkeypatch, n, m, f):
+    """k_om4w (rounds over second-level subtrees, R1 counters per first hop)
+    against the oracle on a ragged batch, with and without the persistent task
+    loop (BA_WAVE_MAX_BLOCKS=1), random faulty sets and given inputs."""
+    from ba_amd import lib as L
+    assert L.load().ba_engine_for(n, m) == L.ENGINE_FUSED
+    B = 64 * 13 + 37
+    kw = dict(seed=0x4A11 + n, faulty_mode=L.FAULTY_RANDOM, f=f, order_mode=L.ORDER_RANDOM,
+              first_trial=64 * 55)
+    od, oo, ocnt = oracle_c.run(n, m, B, **kw)
+    rng = np.random.default_rng(n)
+    fm = (rng.integers(0, 1 << n, B, dtype=np.uint64) & rng.integers(0, 1 << n, B, dtype=np.uint64)
+          ).astype(np.uint32)
+    oc = rng.choice([0, 1, 2], B).astype(np.uint8)
+    gd, go, gcnt = oracle_c.run(n, m, B, seed=3, faulty=fm, order=oc)
+    for cap in (None, "1"):
+        if cap:
+            monkeypatch.setenv("BA_WAVE_MAX_BLOCKS", cap)
+        else:
+            monkeypatch.delenv("BA_WAVE_MAX_BLOCKS", raising=False)
+        e = L.Engine(0)
+        try:
+            res = e.run(n, m, B, engine=L.ENGINE_FUSED, **kw)
+            given = e.run(n, m, B, seed=3, faulty=fm, order=oc, engine=L.ENGINE_FUSED)
+        finally:
+            e.close()
+        tag = f"n={n} m={m} cap={cap}"
+        same(res.decisions, od, "decisions " + tag)
+        same(res.outcome, oo, "outcome " + tag)
+        assert {k: res.counters[k] for k in ocnt} == ocnt, tag
+        same(given.decisions, gd, "given decisions " + tag)
+        same(given.outcome, go, "given outcome " + tag)
+        assert {k: given.counters[k] for k in gcnt} == gcnt, tag
