@@ -120,6 +120,7 @@ struct FusedPlan {
 
 bool leaf_supported(const Geometry& g);
 bool wave_supported(const Geometry& g);
+hipError_t launch_wave_engine(const RunArgs& a, const Geometry& g);
 bool plan_fused(const Geometry& g, FusedPlan& fp);
 hipError_t launch_leaf(const Geometry& g, uint64_t seed, uint64_t gw0, uint32_t W,
                        uint32_t srbase, uint32_t srcnt, const uint64_t* Lm1, const uint64_t* F,

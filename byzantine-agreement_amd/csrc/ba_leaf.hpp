@@ -1,0 +1,91 @@
+// ba_leaf.hpp -- device code shared by the leaf-fused engines (k_leaf,
+// k_fused*, the WAVE kernels): compile-time loops, the leaf-block column
+// majorities, and the diagnostic phase stamps of the lab builds.
+#pragma once
+#include "ba_engine.hpp"
+
+namespace ba {
+
+constexpr int planes_c(int s) { return s < 2 ? 1 : (s < 4 ? 2 : (s < 8 ? 3 : (s < 16 ? 4 : 5))); }
+
+// Compile-time loop: f(std::integral_constant<int, I>) for I in [B, E).  Every
+// register-array index in the leaf code goes through this, so no index is ever
+// dynamic (a dynamic index would send the array to scratch memory).
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+// Column majorities of one leaf block.  diag[a] = L_{me-1}[sigma.j_a] (the
+// direct value, also every loyal row's broadcast), Fm[a] = faulty word of j_a.
+// Column b counts diag[b] then rows a != b in row order, so the carry-save
+// counters see a compile-time input schedule (Csa, ba_device.hpp).
+// The S(S-1)/2 Philox calls run in interleaved groups of PG (philox10_n);
+// each group's 2*PG lie words feed the counters before the next group starts.
+constexpr int leaf_philox_group(int npair) { return npair % 3 == 0 ? 3 : (npair % 4 == 0 ? 4 : (npair % 2 == 0 ? 2 : 3)); }
+
+template <int S>
+__device__ __forceinline__ void leaf_block(uint32_t me, uint64_t seed, uint64_t gw, uint32_t sr,
+                                           const uint64_t (&diag)[S], const uint64_t (&Fm)[S],
+                                           uint64_t (&R)[S]) {
+    constexpr int NL = planes_c(S);
+    constexpr int NPAIR = S * (S - 1) / 2;
+    constexpr int PG = leaf_philox_group(NPAIR);
+    Csa<NL> cnt[S];
+    static_for<0, S>([&](auto b) { cnt[b()].template add<0>(diag[b()]); });
+    const uint32_t pair0 = sr * (uint32_t)NPAIR;  // leaf block base slot sr*S*(S-1) is even
+    static_for<0, (NPAIR + PG - 1) / PG>([&](auto grp) {
+        constexpr int q0 = grp() * PG, ng = NPAIR - q0 < PG ? NPAIR - q0 : PG;
+        uint64_t lw[2 * ng];
+        lie_pairs<ng>(seed, me, pair0 + q0, gw, lw);
+        static_for<0, 2 * ng>([&](auto h) {
+            constexpr int e = 2 * q0 + h();      // slot within the block: row a, column c
+            constexpr int a = e / (S - 1);
+            constexpr int c = e % (S - 1);
+            constexpr int b = c + (c >= a);      // receiver's rank among the S members
+            constexpr int K = 1 + a - (b < a ? 1 : 0);  // inputs column b holds so far
+            cnt[b].template add<K>((Fm[a] & lw[h()]) | (~Fm[a] & diag[a]));
+        });
+    });
+    // S inputs per column; strict majority, inner tie -> non-attack
+    static_for<0, S>([&](auto b) { R[b()] = cnt[b()].template ge<S, S / 2 + 1>(); });
+}
+
+// Bit-sliced count of one matrix column in an LDS word image: the direct value
+// img[diag] plus the child results of rows a != b of prefix sr (s members).
+template <int P>
+__device__ __forceinline__ Count<P> column_count(const uint64_t* img, uint32_t diag,
+                                                 uint32_t child, uint32_t sr, uint32_t s,
+                                                 uint32_t b) {
+    Count<P> cnt;
+    cnt.add(img[diag]);
+    const uint32_t base = child + sr * s * (s - 1);
+    for (uint32_t a = 0; a < b; ++a) cnt.add(img[base + a * (s - 1) + b - 1]);
+    for (uint32_t a = b + 1; a < s; ++a) cnt.add(img[base + a * (s - 1) + b]);
+    return cnt;
+}
+
+// Diagnostic build only (tools/fused_lab.hip defines BA_FUSED_STAMPS): thread 0
+// of every block sums s_memtime cycles per phase; no output depends on them.
+#ifdef BA_FUSED_STAMPS
+__device__ unsigned long long g_fused_stamps[kPartialRows][8];
+#define FUSED_STAMP_INIT() unsigned long long st_prev = __builtin_amdgcn_s_memtime(), st_acc[6] = {0, 0, 0, 0, 0, 0}
+#define FUSED_STAMP(i)                                              \
+    do {                                                            \
+        const unsigned long long st_now = __builtin_amdgcn_s_memtime(); \
+        st_acc[i] += st_now - st_prev;                              \
+        st_prev = st_now;                                           \
+    } while (0)
+#define FUSED_STAMP_STORE()                                                      \
+    if (tid == 0)                                                                \
+        for (int i = 0; i < 6; ++i) g_fused_stamps[blockIdx.x][i] = st_acc[i]
+#else
+#define FUSED_STAMP_INIT()
+#define FUSED_STAMP(i)
+#define FUSED_STAMP_STORE()
+#endif
+
+}  // namespace ba

@@ -1,0 +1,620 @@
+// ba_wave.hpp -- the WAVE engine (gfx950): one wave resolves a task of W
+// 64-trial words alone, walking the OM tree one first-hop (k_om3w, effective
+// depth 3) or second-level (k_om4w, depth 4) subtree per round; see DESIGN.md.
+// Instantiated by ba_wave3.hip / ba_wave4.hip (two translation units, so the
+// two kernel families compile in parallel).
+#pragma once
+#include "ba_leaf.hpp"
+
+namespace ba {
+
+// ---------------------------------------------------------------------------
+// WAVE engine, effective depth 3: each wave owns W consecutive trial words and
+// resolves them alone (no block barrier anywhere; the 4 waves of a block only
+// share the launch).  The tree is walked one first-hop subtree j1 at a time:
+// a subtree has C = L-1 level-1 slots (j1, a), i.e. C leaf blocks, so lane
+// (w, a), w < W = 64 / C, owns leaf block (j1, a) of word w in every round.
+// For n=10 that is 8 words x 8 leaf blocks = all 64 lanes.  Per round:
+//   1. L1[j1, a] = F[j1] ? lie : L0[j1]            (the lane's own leaf parent)
+//   2. leaf block (j1, a): R2[j1, a, *]             (registers -> LDS, S words)
+//   3. lane (w, b = a): R1[j1, b] = maj(L1[j1, b], R2[j1, a', b] : a' != b),
+//      added into the bit-sliced root counter of receiver column j2(b)
+// R1 is never stored: each root column accumulates as the subtrees finish.
+// R2 is stored receiver-major (R2T[w][b][a] = R2[j1, a, b], with the lane's
+// own L1[j1, b] on the diagonal a == b), so step 3 counts C contiguous words
+// with a compile-time carry-save schedule.
+// Lie bits are keyed exactly as in k_fused3 (level, global slot pair, global
+// word), so both kernels give identical results.
+// LDS per wave (uint64 words): IN[W][N+3] (F[N] OB OO VAL) | L0[W][L] |
+// R2T[W][C][C] | RC[W][L][P] (root counters) ; A/U roots reuse R2T when it fits.
+// ---------------------------------------------------------------------------
+// Branch-free synthetic inputs for compile-time N: the same draws as
+// gen_trial (ba_device.hpp), but every Philox call is issued up front, the
+// PK selection steps are predicated and the modes are selects, so the code
+// for several trials is one basic block and their chains interleave.  fm / oc
+// carry the given values in and the resolved ones out.  Valid for
+// min(f, N) <= PK.
+template <int N, int PK>
+__device__ __forceinline__ void gen_trial_u(uint64_t seed, const GenSpec& g, uint64_t t,
+                                            uint32_t& fm, uint32_t& oc) {
+    constexpr int CALLS = (2 + PK + 3) / 4;
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    uint32_t u[4 * CALLS];
+    static_for<0, CALLS>([&](auto c) {
+        const P4 b = philox10(P4{(uint32_t)c(), kGenTag, (uint32_t)t, (uint32_t)(t >> 32)}, k0, k1);
+        u[4 * c()] = b.x;
+        u[4 * c() + 1] = b.y;
+        u[4 * c() + 2] = b.z;
+        u[4 * c() + 3] = b.w;
+    });
+    oc = g.order_mode == 1 ? u[0] >> 31 : (g.order_mode == 2 ? g.order_value : oc);
+    const uint32_t fcap = g.f < (uint32_t)N ? g.f : (uint32_t)N;
+    const uint32_t nf = g.faulty_mode == 1 ? mulhi_range(u[1], fcap + 1) : fcap;
+    // step i takes the j-th (ascending) general not yet chosen: with the
+    // chosen ones kept sorted (s[0] < s[1] < ...), that general is j plus the
+    // number of chosen positions at or below it, found by one compare-increment
+    // per chosen general in ascending order
+    constexpr int NP = PK < N ? PK : N;
+    uint32_t srt[NP > 0 ? NP : 1];
+    uint32_t mask = 0;
+    static_for<0, NP>([&](auto i) {
+        uint32_t pos = mulhi_range(u[2 + i()], (uint32_t)N - i());
+        static_for<0, i()>([&](auto k) { pos += srt[k()] <= pos ? 1u : 0u; });
+        const bool take = (uint32_t)i() < nf;
+        mask |= take ? (1u << pos) : 0u;
+        // insert pos into the sorted list (an untaken step appends N: sorts last)
+        uint32_t x = take ? pos : (uint32_t)N;
+        static_for<0, i()>([&](auto k) {
+            const uint32_t lo = srt[k()] < x ? srt[k()] : x, hi = srt[k()] < x ? x : srt[k()];
+            srt[k()] = lo;
+            x = hi;
+        });
+        srt[i()] = x;
+    });
+    fm = g.faulty_mode != 0 ? mask : fm;
+}
+
+// Inputs of words [0, W) of a wave task -> bit-sliced words in LDS
+// (in[w*NIN + g] = F[g], then OB, OO, VAL).  PK = 0: the generic gen_trial;
+// PK = -1: both inputs given (loads only).
+template <int N, int W, int PK>
+__device__ __forceinline__ void gen_words(uint64_t* in0, uint32_t lane, uint64_t w0, uint64_t seed,
+                                          const GenSpec& gs, uint64_t first_trial, uint64_t batch,
+                                          const uint32_t* __restrict__ faulty,
+                                          const uint8_t* __restrict__ order) {
+    constexpr int NIN = N + 3, G4 = W < 8 ? W : 8;
+    static_for<0, (W + G4 - 1) / G4>([&](auto grp) {
+        constexpr int wb = grp() * G4, nq = W - wb < G4 ? W - wb : G4;
+        uint32_t fm[nq], oc[nq];
+        bool valid[nq];
+        // given inputs first (uniform branches kept out of the draw code)
+        static_for<0, nq>([&](auto q) {
+            const uint64_t i = (w0 + wb + q()) * 64 + lane;
+            valid[q()] = i < batch;
+            fm[q()] = 0;
+            oc[q()] = 0;
+        });
+        if (gs.faulty_mode == 0)
+            static_for<0, nq>([&](auto q) {
+                if (valid[q()]) fm[q()] = faulty[(w0 + wb + q()) * 64 + lane];
+            });
+        if (gs.order_mode == 0)
+            static_for<0, nq>([&](auto q) {
+                if (valid[q()]) oc[q()] = order[(w0 + wb + q()) * 64 + lane];
+            });
+        static_for<0, nq>([&](auto q) {
+            const uint64_t t = first_trial + (w0 + wb + q()) * 64 + lane;
+            if constexpr (PK > 0) gen_trial_u<N, PK>(seed, gs, t, fm[q()], oc[q()]);
+            else if constexpr (PK == 0) {
+                if (valid[q()]) gen_trial(N, seed, gs, t, fm[q()], oc[q()]);
+            }
+        });
+        static_for<0, nq>([&](auto q) {
+            uint64_t mine = 0;
+            static_for<0, N>([&](auto g) {
+                const uint64_t b = __ballot(valid[q()] && ((fm[q()] >> g()) & 1u));
+                if (lane == g()) mine = b;
+            });
+            const uint64_t ob = __ballot(valid[q()] && oc[q()] == 1);
+            const uint64_t oo = __ballot(valid[q()] && oc[q()] == 2);
+            const uint64_t vv = __ballot(valid[q()]);
+            uint64_t* in = in0 + (wb + q()) * NIN;
+            if (lane < (uint32_t)N) in[lane] = mine;
+            if (lane == 0) {
+                in[N] = ob;
+                in[N + 1] = oo;
+                in[N + 2] = vv;
+            }
+        });
+    });
+}
+
+// ---------------------------------------------------------------------------
+// Pieces shared by the WAVE kernels (one wave resolves a task of W words).
+// ---------------------------------------------------------------------------
+// Inputs of a task's W words -> bit-sliced words in0[w*(N+3) + g].
+template <int N, int W, int DIAG>
+__device__ __forceinline__ void wave_inputs(uint64_t* in0, uint32_t lane, uint64_t w0,
+                                            uint64_t seed, const GenSpec& gs,
+                                            uint64_t first_trial, uint64_t batch,
+                                            const uint32_t* __restrict__ faulty,
+                                            const uint8_t* __restrict__ order) {
+    constexpr int NIN = N + 3;
+    const uint32_t pk = gs.faulty_mode == 0 ? 0u : (gs.f < (uint32_t)N ? gs.f : (uint32_t)N);
+    if (gs.faulty_mode == 0 && gs.order_mode == 0) {  // staged inputs: loads only
+        gen_words<N, W, -1>(in0, lane, w0, seed, gs, first_trial, batch, faulty, order);
+    } else if constexpr ((DIAG & 16) != 0) {  // lab: near-free stand-in inputs
+        static_for<0, W>([&](auto wq) {
+            const uint64_t h = (w0 + wq() + 1) * 0x9E3779B97F4A7C15ull;
+            if (lane < (uint32_t)NIN) in0[wq() * NIN + lane] = lane == N + 2 ? ~0ull : (h >> lane) & (h << 3);
+        });
+    } else if (pk <= 2) gen_words<N, W, 2>(in0, lane, w0, seed, gs, first_trial, batch, faulty, order);
+    else if (pk <= 3) gen_words<N, W, 3>(in0, lane, w0, seed, gs, first_trial, batch, faulty, order);
+    else if (pk <= 6) gen_words<N, W, 6>(in0, lane, w0, seed, gs, first_trial, batch, faulty, order);
+    else gen_words<N, W, 0>(in0, lane, w0, seed, gs, first_trial, batch, faulty, order);
+}
+
+// Level 0 of W words (one Philox per slot pair) into l0[w*L + j], and the
+// root counters rc[(w*L + j)*P + q] initialised with it (plane 0 = L0).
+template <int N, int W, int P>
+__device__ __forceinline__ void wave_level0(const uint64_t* in0, uint64_t* l0, uint64_t* rc,
+                                            uint32_t lane, uint64_t seed, uint64_t gw0) {
+    constexpr int L = N - 1, NIN = N + 3;
+    constexpr uint32_t NP0 = (L + 1) / 2;
+    for (uint32_t it = lane; it < (uint32_t)W * NP0; it += 64) {
+        const uint32_t w = it / NP0, p = it - w * NP0;
+        const uint64_t* in = in0 + w * NIN;
+        const uint64_t F0 = in[0], ob = in[N];
+        uint64_t lv[2];
+        lie_pair(seed, 0, p, gw0 + w, lv[0], lv[1]);
+        static_for<0, 2>([&](auto h) {
+            const uint32_t j = 2 * p + h();
+            if (j < (uint32_t)L) {
+                const uint64_t v = (F0 & lv[h()]) | (~F0 & ob);
+                l0[w * L + j] = v;
+                uint64_t* c = rc + (w * L + j) * P;
+                c[0] = v;
+                static_for<1, P>([&](auto q) { c[q()] = 0; });
+            }
+        });
+    }
+}
+
+// c[0..P) (bit-sliced planes in LDS) += x
+template <int P>
+__device__ __forceinline__ void planes_add(uint64_t* c, uint64_t x) {
+    static_for<0, P>([&](auto q) {
+        const uint64_t v = c[q()];
+        c[q()] = v ^ x;
+        x &= v;
+    });
+}
+
+// Root majorities of W words from the root counters (L inputs each): strict
+// majority attacks, a tie is "undefined" (ba.py:188-195).  au[w*2L + b] = A,
+// au[w*2L + L + b] = U.
+template <int L, int W, int P>
+__device__ __forceinline__ void wave_roots(const uint64_t* rc, uint64_t* au, uint32_t lane) {
+    for (uint32_t it = lane; it < (uint32_t)W * L; it += 64) {
+        const uint32_t w = it / L, col = it - w * L;
+        const uint64_t* c = rc + (w * L + col) * P;
+        Count<P> cnt;
+        static_for<0, P>([&](auto q) { cnt.c[q()] = c[q()]; });
+        const uint64_t att = cnt.ge(L / 2 + 1);
+        const uint64_t tie = (L & 1) ? 0ull : (cnt.ge(L / 2) & ~att);
+        au[w * 2 * L + col] = att;
+        au[w * 2 * L + L + col] = tie;
+    }
+}
+
+// Per-trial epilogue (lane = trial) of W words, two words per iteration:
+// their LDS reads and logic interleave without the register blow-up (and
+// spills) of unrolling all W words at once.
+template <int N, int W, uint32_t ME, int DIAG>
+__device__ __forceinline__ void wave_epilogue(const uint64_t* in0, const uint64_t* au0,
+                                              uint32_t lane, uint64_t w0, uint64_t batch,
+                                              uint64_t* __restrict__ decisions,
+                                              uint8_t* __restrict__ outcome, TrialCounts& tc) {
+    constexpr int L = N - 1, NIN = N + 3;
+    if constexpr ((DIAG & 32) != 0) {  // lab: near-free stand-in epilogue
+        static_for<0, W>([&](auto wq) {
+            const uint64_t i = (w0 + wq()) * 64 + lane;
+            if (i < batch) decisions[i] = au0[wq() * 2 * L + (lane & 15)];
+        });
+        return;
+    }
+    constexpr int EW = 2;
+#pragma unroll 1
+    for (int wb = 0; wb < W; wb += EW) {
+        uint64_t dec_out[EW];
+        uint32_t out_out[EW];
+        static_for<0, EW>([&](auto wq) {
+            const int w = wb + wq();
+            out_out[wq()] = 0xFFu;  // 0xFF: not a trial of this batch
+            dec_out[wq()] = 0;
+            if (W % EW != 0 && w >= W) return;
+            const uint64_t* inw = in0 + w * NIN;
+            const uint64_t* au = au0 + w * 2 * L;
+            const bool live = (inw[N + 2] >> lane) & 1ull;
+            uint32_t A = 0, U = 0, fm = 0;
+            static_for<0, L>([&](auto b) {
+                A |= (uint32_t)((au[b()] >> lane) & 1ull) << (b() + 1);
+                U |= (uint32_t)((au[L + b()] >> lane) & 1ull) << (b() + 1);
+            });
+            static_for<0, N>([&](auto g) { fm |= (uint32_t)((inw[g()] >> lane) & 1ull) << g(); });
+            const uint32_t ob = (uint32_t)(inw[N] >> lane) & 1u;
+            const uint32_t oo = (uint32_t)(inw[N + 1] >> lane) & 1u;
+            const TrialResult r = trial_result(N, ME, fm, oo ? 2u : ob, A, U);
+            const uint32_t lv = live ? 1u : 0u;
+            const uint32_t q = r.out & 3, agree = (r.out >> 2) & 1, appl = (r.out >> 3) & 1;
+            const uint32_t valid = (r.out >> 4) & 1, inb = (r.out >> 5) & 1;
+            tc.v[C_TRIALS] += lv;
+            tc.v[C_AGREE] += lv & agree;
+            tc.v[C_VAPPL] += lv & appl;
+            tc.v[C_VALID] += lv & valid;
+            tc.v[C_QR] += lv & (q == 0);
+            tc.v[C_QA] += lv & (q == 1);
+            tc.v[C_QU] += lv & (q == 2);
+            tc.v[C_UNDEF] += lv * r.nU;
+            tc.v[C_INB] += lv & inb;
+            tc.v[C_VIOL] += lv & inb & ((agree ^ 1u) | (appl & (valid ^ 1u)));
+            tc.v[C_FTOT] += lv * r.nf;
+            tc.v[C_ATT] += lv * r.nA;
+            dec_out[wq()] = r.dec;
+            out_out[wq()] = live ? r.out : 0xFFu;
+        });
+        static_for<0, EW>([&](auto wq) {
+            const uint64_t i = (w0 + wb + wq()) * 64 + lane;
+            if (out_out[wq()] != 0xFFu) {
+                if (!(DIAG & 1) && decisions) decisions[i] = dec_out[wq()];
+                if (!(DIAG & 2) && outcome) outcome[i] = (uint8_t)out_out[wq()];
+            }
+        });
+    }
+}
+
+// Run counters of the block: wave sums (lane c holds counter c), the waves
+// combine in LDS, then one sink unit per block.  Every wave of the block
+// must call it (it contains a block barrier).
+__device__ __forceinline__ void wave_flush(const TrialCounts& tc, uint32_t lane, uint32_t wv,
+                                           uint32_t wpb, uint64_t* __restrict__ counters,
+                                           const Sink& sk, bool skip) {
+    uint64_t mine = 0;
+#pragma unroll
+    for (int c = 0; c < C_NUM; ++c) {
+        uint32_t x = tc.v[c];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+        if (lane == (uint32_t)c) mine = x;
+    }
+    __shared__ unsigned long long wcnt[kWaveThreads / 64][16];
+    if (lane < 16) wcnt[wv][lane] = mine;
+    __syncthreads();
+    if (wv == 0 && !skip) {
+        uint64_t tot = 0;
+        for (uint32_t k = 0; k < wpb; ++k) tot += lane < 16 ? wcnt[k][lane] : 0;
+        sink_counters(lane, tot, blockIdx.x, gridDim.x, counters, sk);
+    }
+}
+
+// Issue priority of the two waves sharing a SIMD alternates every round
+// (wave slot parity): with equal priority the older wave takes nearly every
+// VALU slot and the younger one finishes its task alone.
+__device__ __forceinline__ void wave_alternate_priority(uint32_t round) {
+    const uint32_t slot = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (3 << 11)) & 1u;
+    if (((round + slot) & 1u) != 0) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
+
+// ---------------------------------------------------------------------------
+// k_om3w: effective depth 3 (see the WAVE engine note above)
+// ---------------------------------------------------------------------------
+template <int N>
+struct Om3W {
+    static constexpr int L = N - 1, S = N - 3, C = L - 1;
+    static constexpr int W = 64 / C;               // trial words per wave task
+    static constexpr int LANES = W * C;            // lanes busy in the subtree rounds
+    static constexpr int P = planes_c(L);          // root counter planes (L inputs)
+    static constexpr int NIN = N + 3;
+    static constexpr int oIN = 0, oL0 = oIN + W * NIN, oR2 = oL0 + W * L, oRC = oR2 + W * C * C;
+    static constexpr int end0 = oRC + W * L * P;
+    static constexpr bool au_in_r2 = 2 * L <= C * C;
+    static constexpr int oAU = au_in_r2 ? oR2 : end0;
+    static constexpr int words = ((au_in_r2 ? end0 : end0 + W * 2 * L) + 1) & ~1;
+};
+
+// DIAG: lab-only ablation switches (tools/om3_lab.hip); the product uses 0.
+template <int N, int DIAG = 0>
+__global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
+    uint64_t seed, GenSpec gs, uint64_t first_trial, uint64_t batch,
+    const uint32_t* __restrict__ faulty, const uint8_t* __restrict__ order,
+    uint64_t* __restrict__ decisions, uint8_t* __restrict__ outcome,
+    uint64_t* __restrict__ counters, Sink sk) {
+    using G = Om3W<N>;
+    constexpr int L = G::L, S = G::S, C = G::C, W = G::W, P = G::P, NIN = G::NIN;
+    constexpr uint32_t ME = 3;
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    uint64_t* img = lds + (uint64_t)wv * G::words;
+    const uint64_t total_words = (batch + 63) / 64;
+    const uint64_t ntasks = (total_words + W - 1) / W;
+    // this lane's (word, leaf block) in the subtree rounds
+    const uint32_t lw_ = lane / C, la = lane - lw_ * C;
+    const bool act = lane < (uint32_t)G::LANES;
+    const uint32_t lw = act ? lw_ : 0;
+    TrialCounts tc;
+    FUSED_STAMP_INIT();
+#ifdef BA_FUSED_STAMPS
+    const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    for (uint64_t task = (uint64_t)blockIdx.x * wpb + wv; task < ntasks;
+         task += (uint64_t)gridDim.x * wpb) {
+        const uint64_t w0 = task * W;
+        const uint64_t gw0 = (first_trial >> 6) + w0;
+        wave_inputs<N, W, DIAG>(img + G::oIN, lane, w0, seed, gs, first_trial, batch, faulty, order);
+        __builtin_amdgcn_wave_barrier();
+        FUSED_STAMP(0);
+        wave_level0<N, W, P>(img + G::oIN, img + G::oL0, img + G::oRC, lane, seed, gw0);
+        __builtin_amdgcn_wave_barrier();
+        // ---- subtree rounds ------------------------------------------------------
+        const uint64_t* in = img + G::oIN + lw * NIN;
+        const uint64_t gw = gw0 + lw;
+        for (uint32_t j1 = 0; j1 < (uint32_t)L; ++j1) {
+            if constexpr ((DIAG & 8) == 0) wave_alternate_priority(j1);
+            const uint32_t sr = j1 * C + la;             // level-1 slot (j1, j2)
+            const uint32_t j2 = la + (la >= j1);
+            uint64_t par = 0;
+            if (act) {
+                // 1. L1[j1, a] (sender j1 relays L0[j1]) and the level-2 diagonal
+                //    pairs of leaf block (j1, a): one interleaved Philox group
+                const uint32_t x0 = sr * S;
+                constexpr int NPD = (S + 1) / 2;
+                P4 pc[NPD + 1];
+                static_for<0, NPD>([&](auto qd) {
+                    pc[qd()] = P4{(x0 >> 1) + qd(), 2u, (uint32_t)gw, (uint32_t)(gw >> 32)};
+                });
+                pc[NPD] = P4{sr >> 1, 1u, (uint32_t)gw, (uint32_t)(gw >> 32)};
+                philox10_n<NPD + 1>(pc, (uint32_t)seed, (uint32_t)(seed >> 32));
+                uint64_t lw2[2 * NPD];
+                static_for<0, NPD>([&](auto qd) {
+                    lw2[2 * qd()] = (uint64_t)pc[qd()].y << 32 | pc[qd()].x;
+                    lw2[2 * qd() + 1] = (uint64_t)pc[qd()].w << 32 | pc[qd()].z;
+                });
+                const uint64_t lie = (sr & 1u) ? ((uint64_t)pc[NPD].w << 32 | pc[NPD].z)
+                                               : ((uint64_t)pc[NPD].y << 32 | pc[NPD].x);
+                const uint64_t fj = in[j1 + 1];
+                par = (fj & lie) | (~fj & img[G::oL0 + lw * L + j1]);
+                // 2. leaf block (j1, a): level-2 diagonal, then S(S-1) leaves
+                const uint32_t lo = j1 < j2 ? j1 : j2, hi = j1 < j2 ? j2 : j1;
+                const uint64_t fs = in[j2 + 1];  // level-2 sender: j2
+                const uint64_t oddmask = 0ull - (uint64_t)(x0 & 1u);
+                uint64_t diag[S], Fm[S], R[S];
+                static_for<0, S>([&](auto a) {
+                    uint64_t lie2;
+                    if constexpr (S % 2 == 1) lie2 = lw2[a()] ^ ((lw2[a()] ^ lw2[a() + 1]) & oddmask);
+                    else lie2 = lw2[a()];
+                    diag[a()] = (fs & lie2) | (~fs & par);
+                    const uint32_t ida = a() + (a() >= lo) + (a() + 1 >= hi);  // member a's rank
+                    Fm[a()] = in[ida + 1];
+                });
+                leaf_block<S>(ME, seed, gw, sr, diag, Fm, R);
+                // receiver-major: member d of block a is receiver b = d + (d >= a)
+                uint64_t* r2t = img + G::oR2 + lw * C * C + la;
+                r2t[la * C] = par;
+                static_for<0, S>([&](auto d) { r2t[(d() + (d() >= la ? 1u : 0u)) * C] = R[d()]; });
+            }
+            __builtin_amdgcn_wave_barrier();
+            FUSED_STAMP(1);
+            if (act) {
+                // 3. R1[j1, b], b = la: L1[j1, b] (this lane's own parent) plus
+                //    column b of the word's other leaf blocks a' != b
+                const uint64_t* col = img + G::oR2 + (lw * C + la) * C;
+                Csa<planes_c(C)> cnt;
+                static_for<0, C>([&](auto a) { cnt.template add<a()>(col[a()]); });
+                const uint64_t r1 = cnt.template ge<C, C / 2 + 1>();  // inner tie -> non-attack
+                // root column j2 += R1[j1, b] (ripple add on the bit-sliced planes)
+                planes_add<P>(img + G::oRC + (lw * L + j2) * P, r1);
+            }
+            __builtin_amdgcn_wave_barrier();
+            FUSED_STAMP(2);
+        }
+        wave_roots<L, W, P>(img + G::oRC, img + G::oAU, lane);
+        __builtin_amdgcn_wave_barrier();
+        FUSED_STAMP(3);
+        wave_epilogue<N, W, ME, DIAG>(img + G::oIN, img + G::oAU, lane, w0, batch, decisions,
+                                      outcome, tc);
+        __builtin_amdgcn_wave_barrier();
+        FUSED_STAMP(4);
+    }
+    wave_flush(tc, lane, wv, wpb, counters, sk, (DIAG & 4) != 0);
+#ifdef BA_FUSED_STAMPS
+    if (lane == 0 && blockIdx.x * wpb + wv < (uint32_t)kPartialRows)
+    {
+        for (int i = 0; i < 6; ++i) g_fused_stamps[blockIdx.x * wpb + wv][i] = st_acc[i];
+        g_fused_stamps[blockIdx.x * wpb + wv][6] = rt0;
+        // [5]: HW_ID | XCC_ID << 32 (s_getreg: id | offset << 6 | (size - 1) << 11)
+        g_fused_stamps[blockIdx.x * wpb + wv][5] =
+            __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11)) |
+            ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (31 << 11)) << 32);
+        g_fused_stamps[blockIdx.x * wpb + wv][7] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// k_om4w: effective depth 4 (n=13, m=4 is SURVEY config 3).  Same wave-task
+// design one level deeper: a round is a second-level subtree (j1, j2), whose
+// C2 = L-2 level-2 slots (j1, j2, a) are C2 leaf blocks, so lane (w, a),
+// w < W = 64 / C2, owns leaf block (j1, j2, a) of word w.  Per round:
+//   1. one interleaved Philox group: L1[j1, j2], L2[j1, j2, a] (the lane's
+//      leaf parent) and the level-3 diagonal pairs of its block
+//   2. leaf block: R3[j1, j2, a, *] into LDS receiver-major (L2 on the
+//      diagonal), as R2 in k_om3w
+//   3. lane (w, b): R2[j1, j2, b] = maj over C2 contiguous words (carry-save),
+//      added into the R1 counter of (w, j1, receiver), and L1[j1, j2] into
+//      the R1 counter of (w, j1, j2)
+// After the C1 = L-1 rounds of j1, R1[j1, c] (strict majority of C1 inputs)
+// is added into the root counters; roots and epilogue are k_om3w's.
+// LDS per wave: IN[W][N+3] | L0[W][L] | R3T[W][C2][C2] | R1C[W][C1][P1] |
+// RC[W][L][P] ; A/U roots reuse R3T when it fits.
+// ---------------------------------------------------------------------------
+template <int N>
+struct Om4W {
+    static constexpr int L = N - 1, S = N - 4, C1 = L - 1, C2 = L - 2;
+    static constexpr int W = 64 / C2;
+    static constexpr int LANES = W * C2;
+    static constexpr int P = planes_c(L), P1 = planes_c(C1);
+    static constexpr int NIN = N + 3;
+    static constexpr int oIN = 0, oL0 = oIN + W * NIN, oR3 = oL0 + W * L;
+    static constexpr int oR1 = oR3 + W * C2 * C2, oRC = oR1 + W * C1 * P1;
+    static constexpr int end0 = oRC + W * L * P;
+    static constexpr bool au_in_r3 = 2 * L <= C2 * C2;
+    static constexpr int oAU = au_in_r3 ? oR3 : end0;
+    static constexpr int words = ((au_in_r3 ? end0 : end0 + W * 2 * L) + 1) & ~1;
+};
+
+template <int N>
+__global__ __launch_bounds__(kWaveThreads, 2) void k_om4w(
+    uint64_t seed, GenSpec gs, uint64_t first_trial, uint64_t batch,
+    const uint32_t* __restrict__ faulty, const uint8_t* __restrict__ order,
+    uint64_t* __restrict__ decisions, uint8_t* __restrict__ outcome,
+    uint64_t* __restrict__ counters, Sink sk) {
+    using G = Om4W<N>;
+    constexpr int L = G::L, S = G::S, C1 = G::C1, C2 = G::C2, W = G::W, P = G::P, P1 = G::P1;
+    constexpr int NIN = G::NIN;
+    constexpr uint32_t ME = 4;
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    uint64_t* img = lds + (uint64_t)wv * G::words;
+    const uint64_t total_words = (batch + 63) / 64;
+    const uint64_t ntasks = (total_words + W - 1) / W;
+    const uint32_t lw_ = lane / C2, la = lane - lw_ * C2;
+    const bool act = lane < (uint32_t)G::LANES;
+    const uint32_t lw = act ? lw_ : 0;
+    TrialCounts tc;
+    for (uint64_t task = (uint64_t)blockIdx.x * wpb + wv; task < ntasks;
+         task += (uint64_t)gridDim.x * wpb) {
+        const uint64_t w0 = task * W;
+        const uint64_t gw0 = (first_trial >> 6) + w0;
+        wave_inputs<N, W, 0>(img + G::oIN, lane, w0, seed, gs, first_trial, batch, faulty, order);
+        __builtin_amdgcn_wave_barrier();
+        wave_level0<N, W, P>(img + G::oIN, img + G::oL0, img + G::oRC, lane, seed, gw0);
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t* in = img + G::oIN + lw * NIN;
+        const uint64_t gw = gw0 + lw;
+        uint32_t round = 0;
+        for (uint32_t j1 = 0; j1 < (uint32_t)L; ++j1) {
+            // R1 counters of this j1 start at zero
+            for (uint32_t it = lane; it < (uint32_t)(W * C1 * P1); it += 64) img[G::oR1 + it] = 0;
+            __builtin_amdgcn_wave_barrier();
+            const uint64_t fj1 = in[j1 + 1];
+            const uint64_t l0j1 = img[G::oL0 + lw * L + j1];
+            for (uint32_t c2 = 0; c2 < (uint32_t)C1; ++c2, ++round) {
+                wave_alternate_priority(round);
+                const uint32_t j2 = c2 + (c2 >= j1);
+                const uint32_t lo = j1 < j2 ? j1 : j2, hi = j1 < j2 ? j2 : j1;
+                const uint32_t x1 = j1 * C1 + c2;     // level-1 slot (j1, j2)
+                const uint32_t x2 = x1 * C2 + la;     // level-2 slot (j1, j2, j3): leaf block
+                const uint32_t j3 = la + (la >= lo) + (la + 1 >= hi);  // the a-th other lieutenant
+                uint64_t par = 0, l1v = 0;
+                if (act) {
+                    const uint32_t x3 = x2 * S;
+                    constexpr int NPD = (S + 1) / 2;
+                    P4 pc[NPD + 2];
+                    static_for<0, NPD>([&](auto qd) {
+                        pc[qd()] = P4{(x3 >> 1) + qd(), 3u, (uint32_t)gw, (uint32_t)(gw >> 32)};
+                    });
+                    pc[NPD] = P4{x2 >> 1, 2u, (uint32_t)gw, (uint32_t)(gw >> 32)};
+                    pc[NPD + 1] = P4{x1 >> 1, 1u, (uint32_t)gw, (uint32_t)(gw >> 32)};
+                    philox10_n<NPD + 2>(pc, (uint32_t)seed, (uint32_t)(seed >> 32));
+                    uint64_t lw3[2 * NPD];
+                    static_for<0, NPD>([&](auto qd) {
+                        lw3[2 * qd()] = (uint64_t)pc[qd()].y << 32 | pc[qd()].x;
+                        lw3[2 * qd() + 1] = (uint64_t)pc[qd()].w << 32 | pc[qd()].z;
+                    });
+                    const uint64_t lie2 = (x2 & 1u) ? ((uint64_t)pc[NPD].w << 32 | pc[NPD].z)
+                                                    : ((uint64_t)pc[NPD].y << 32 | pc[NPD].x);
+                    const uint64_t lie1 = (x1 & 1u) ? ((uint64_t)pc[NPD + 1].w << 32 | pc[NPD + 1].z)
+                                                    : ((uint64_t)pc[NPD + 1].y << 32 | pc[NPD + 1].x);
+                    l1v = (fj1 & lie1) | (~fj1 & l0j1);              // L1[j1, j2], sender j1
+                    const uint64_t fj2 = in[j2 + 1];
+                    par = (fj2 & lie2) | (~fj2 & l1v);               // L2[j1, j2, j3], sender j2
+                    // members of leaf block (j1, j2, j3): the lieutenants not in
+                    // {j1, j2, j3}, ascending
+                    const uint32_t e0 = lo < j3 ? lo : j3;
+                    const uint32_t e2 = hi > j3 ? hi : j3;
+                    const uint32_t e1 = lo + hi + j3 - e0 - e2;
+                    const uint64_t fs = in[j3 + 1];  // level-3 sender: j3
+                    const uint64_t oddmask = 0ull - (uint64_t)(x3 & 1u);
+                    uint64_t diag[S], Fm[S], R[S];
+                    static_for<0, S>([&](auto d) {
+                        uint64_t lie3;
+                        if constexpr (S % 2 == 1) lie3 = lw3[d()] ^ ((lw3[d()] ^ lw3[d() + 1]) & oddmask);
+                        else lie3 = lw3[d()];
+                        diag[d()] = (fs & lie3) | (~fs & par);
+                        uint32_t m = d();
+                        m += m >= e0 ? 1u : 0u;
+                        m += m >= e1 ? 1u : 0u;
+                        m += m >= e2 ? 1u : 0u;
+                        Fm[d()] = in[m + 1];
+                    });
+                    leaf_block<S>(ME, seed, gw, x2, diag, Fm, R);
+                    uint64_t* r3t = img + G::oR3 + lw * C2 * C2 + la;
+                    r3t[la * C2] = par;
+                    static_for<0, S>([&](auto d) { r3t[(d() + (d() >= la ? 1u : 0u)) * C2] = R[d()]; });
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (act) {
+                    // R2[j1, j2, b], b = la (receiver: the la-th lieutenant not in {j1, j2})
+                    const uint64_t* col = img + G::oR3 + (lw * C2 + la) * C2;
+                    Csa<planes_c(C2)> cnt;
+                    static_for<0, C2>([&](auto a) { cnt.template add<a()>(col[a()]); });
+                    const uint64_t r2 = cnt.template ge<C2, C2 / 2 + 1>();  // inner tie -> non-attack
+                    // receiver j3 (same formula as above) as a rank among the non-j1
+                    planes_add<P1>(img + G::oR1 + (lw * C1 + (j3 - (j3 > j1 ? 1u : 0u))) * P1, r2);
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (act && la == 0) planes_add<P1>(img + G::oR1 + (lw * C1 + c2) * P1, l1v);
+                __builtin_amdgcn_wave_barrier();
+            }
+            // R1[j1, c] -> root column c (rank among the non-j1) -> general rank
+            for (uint32_t it = lane; it < (uint32_t)(W * C1); it += 64) {
+                const uint32_t w = it / C1, c = it - w * C1;
+                const uint64_t* r1c = img + G::oR1 + (w * C1 + c) * P1;
+                Count<P1> cnt;
+                static_for<0, P1>([&](auto q) { cnt.c[q()] = r1c[q()]; });
+                const uint64_t r1 = cnt.ge(C1 / 2 + 1);  // inner tie -> non-attack
+                planes_add<P>(img + G::oRC + (w * L + c + (c >= j1 ? 1u : 0u)) * P, r1);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        wave_roots<L, W, P>(img + G::oRC, img + G::oAU, lane);
+        __builtin_amdgcn_wave_barrier();
+        wave_epilogue<N, W, ME, 0>(img + G::oIN, img + G::oAU, lane, w0, batch, decisions, outcome, tc);
+        __builtin_amdgcn_wave_barrier();
+    }
+    wave_flush(tc, lane, wv, wpb, counters, sk, false);
+}
+
+// WAVE engine launch: one wave per W-word task, 4 independent waves per block,
+// at most two blocks per CU (two waves per SIMD, the kernels' register budget)
+// and a persistent task loop.
+template <typename G, typename K>
+inline hipError_t launch_wave(const RunArgs& a, K kernel, const char* name) {
+    constexpr uint32_t wpb = kWaveThreads / 64;
+    const uint64_t words = (a.batch + 63) / 64, tasks = (words + G::W - 1) / G::W;
+    uint64_t blocks = (tasks + wpb - 1) / wpb;
+    uint64_t cap = 2ull * a.cu_count;
+    if (const char* e = getenv("BA_WAVE_MAX_BLOCKS")) {  // tests: force the persistent task loop
+        const uint64_t c = strtoull(e, nullptr, 0);
+        if (c >= 1 && c < cap) cap = c;
+    }
+    if (blocks > cap) blocks = cap;
+    ProfScope ps(a.prof, name, a.stream);
+    hipLaunchKernelGGL(kernel, dim3((uint32_t)blocks), dim3(kWaveThreads), wpb * G::words * 8,
+                       a.stream, a.seed, a.gen, a.first_trial, a.batch, a.faulty, a.order,
+                       a.decisions, a.outcome, a.counters, a.sink);
+    return hipGetLastError();
+}
+
+}  // namespace ba

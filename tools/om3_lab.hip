@@ -6,6 +6,8 @@
 //   run:   tools/om3_lab [batch]
 #define BA_FUSED_STAMPS 1
 #include "../byzantine-agreement_amd/csrc/ba_fused.hip"
+#include "../byzantine-agreement_amd/csrc/ba_wave3.hip"
+#include "../byzantine-agreement_amd/csrc/ba_wave4.hip"
 #include "../byzantine-agreement_amd/csrc/ba_levels.hip"
 
 #include <cstdio>
