@@ -358,6 +358,29 @@ static int compare_wave(uint64_t B) {
         for (auto& kv : hist_simd) printf("\"%d\": %d, ", kv.first, kv.second);
         printf("}, \"dur_p10\": %.1f, \"dur_p50\": %.1f, \"dur_p90\": %.1f}\n", d[d.size() / 10].first,
                d[d.size() / 2].first, d[d.size() * 9 / 10].first);
+        // the two waves of each SIMD: wave slot ids (HW_ID[3:0]) and who finishes first
+        std::map<unsigned long long, std::vector<std::pair<int, double>>> bysimd;
+        for (auto& x : d) {
+            const unsigned long long h = x.second;
+            const unsigned long long cu = ((h >> 8) & 15) | ((h >> 12) & 1) << 4 | ((h >> 13) & 7) << 5 | (h >> 32 & 15) << 8;
+            bysimd[cu << 2 | ((h >> 4) & 3)].push_back({(int)(h & 15), x.first});
+        }
+        int pairs = 0, diffpar = 0, lowfirst = 0;
+        std::map<int, int> slots;
+        for (auto& kv : bysimd) {
+            if (kv.second.size() != 2) continue;
+            ++pairs;
+            auto a = kv.second[0], b = kv.second[1];
+            slots[a.first]++;
+            slots[b.first]++;
+            diffpar += (a.first & 1) != (b.first & 1);
+            const auto& fast = a.second < b.second ? a : b;
+            const auto& slow = a.second < b.second ? b : a;
+            lowfirst += fast.first < slow.first;
+        }
+        printf("{\"simd_pairs\": %d, \"diff_slot_parity\": %d, \"lower_slot_finishes_first\": %d, \"slot_hist\": {", pairs, diffpar, lowfirst);
+        for (auto& kv : slots) printf("\"%d\": %d, ", kv.first, kv.second);
+        printf("}}\n");
     }
     printf("{\"clock_ghz\": %.3f, \"span_us\": %.2f, \"start_skew_us\": %.2f, \"first_end_us\": %.2f, "
            "\"mean_wave_us\": %.2f}\n",
