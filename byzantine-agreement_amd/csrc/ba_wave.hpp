@@ -369,19 +369,50 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
                 //    pairs of leaf block (j1, a): one interleaved Philox group
                 const uint32_t x0 = sr * S;
                 constexpr int NPD = (S + 1) / 2;
-                P4 pc[NPD + 1];
-                static_for<0, NPD>([&](auto qd) {
-                    pc[qd()] = P4{(x0 >> 1) + qd(), 2u, (uint32_t)gw, (uint32_t)(gw >> 32)};
-                });
-                pc[NPD] = P4{sr >> 1, 1u, (uint32_t)gw, (uint32_t)(gw >> 32)};
-                philox10_n<NPD + 1>(pc, (uint32_t)seed, (uint32_t)(seed >> 32));
-                uint64_t lw2[2 * NPD];
-                static_for<0, NPD>([&](auto qd) {
-                    lw2[2 * qd()] = (uint64_t)pc[qd()].y << 32 | pc[qd()].x;
-                    lw2[2 * qd() + 1] = (uint64_t)pc[qd()].w << 32 | pc[qd()].z;
-                });
-                const uint64_t lie = (sr & 1u) ? ((uint64_t)pc[NPD].w << 32 | pc[NPD].z)
-                                               : ((uint64_t)pc[NPD].y << 32 | pc[NPD].x);
+                uint64_t lw2[2 * NPD], lie;
+                if constexpr (S % 2 == 1 && C % 2 == 0) {
+                    // Lanes a, a^1 hold leaf blocks sr even / odd of one word: they
+                    // share the level-1 pair sr>>1 and one level-2 pair (the even
+                    // block's last = the odd block's first), 2*NPD distinct calls
+                    // for the two.  Each lane issues NPD of them and takes the
+                    // missing one from its partner: the even lane the shared
+                    // level-2 pair, the odd lane the level-1 pair.
+                    const bool odd = (sr & 1u) != 0;
+                    const uint32_t d0 = x0 >> 1;  // first level-2 pair of this block
+                    P4 pc[NPD];
+                    static_for<0, NPD>([&](auto qd) {
+                        const bool l1 = !odd && qd() == NPD - 1;
+                        pc[qd()] = P4{l1 ? (sr >> 1) : d0 + qd(), l1 ? 1u : 2u, (uint32_t)gw,
+                                      (uint32_t)(gw >> 32)};
+                    });
+                    philox10_n<NPD>(pc, (uint32_t)seed, (uint32_t)(seed >> 32));
+                    // even lane sends its level-1 pair, odd lane its first level-2 pair
+                    P4 snd = odd ? pc[0] : pc[NPD - 1], rcv;
+                    rcv.x = __shfl_xor(snd.x, 1, 64);
+                    rcv.y = __shfl_xor(snd.y, 1, 64);
+                    rcv.z = __shfl_xor(snd.z, 1, 64);
+                    rcv.w = __shfl_xor(snd.w, 1, 64);
+                    const P4 p1 = odd ? rcv : pc[NPD - 1];
+                    static_for<0, NPD>([&](auto qd) {
+                        const P4 q = (qd() == NPD - 1 && !odd) ? rcv : pc[qd()];
+                        lw2[2 * qd()] = (uint64_t)q.y << 32 | q.x;
+                        lw2[2 * qd() + 1] = (uint64_t)q.w << 32 | q.z;
+                    });
+                    lie = odd ? ((uint64_t)p1.w << 32 | p1.z) : ((uint64_t)p1.y << 32 | p1.x);
+                } else {
+                    P4 pc[NPD + 1];
+                    static_for<0, NPD>([&](auto qd) {
+                        pc[qd()] = P4{(x0 >> 1) + qd(), 2u, (uint32_t)gw, (uint32_t)(gw >> 32)};
+                    });
+                    pc[NPD] = P4{sr >> 1, 1u, (uint32_t)gw, (uint32_t)(gw >> 32)};
+                    philox10_n<NPD + 1>(pc, (uint32_t)seed, (uint32_t)(seed >> 32));
+                    static_for<0, NPD>([&](auto qd) {
+                        lw2[2 * qd()] = (uint64_t)pc[qd()].y << 32 | pc[qd()].x;
+                        lw2[2 * qd() + 1] = (uint64_t)pc[qd()].w << 32 | pc[qd()].z;
+                    });
+                    lie = (sr & 1u) ? ((uint64_t)pc[NPD].w << 32 | pc[NPD].z)
+                                    : ((uint64_t)pc[NPD].y << 32 | pc[NPD].x);
+                }
                 const uint64_t fj = in[j1 + 1];
                 par = (fj & lie) | (~fj & img[G::oL0 + lw * L + j1]);
                 // 2. leaf block (j1, a): level-2 diagonal, then S(S-1) leaves
