@@ -396,3 +396,37 @@ def test_om4_wave_vs_oracle(monkeypatch, n, m, f):
         same(given.decisions, gd, "given decisions " + tag)
         same(given.outcome, go, "given outcome " + tag)
         assert {k: given.counters[k] for k in gcnt} == gcnt, tag
+
+
+def test_random_configs_fuzz(engine):
+    """30 seeded random (n, m, f, modes, batch, first_trial) cases on the AUTO
+    engine, each bit-exact against the oracle (decisions, outcomes, counters)."""
+    from ba_amd import lib as L
+    rng = np.random.default_rng(20261016)
+    for case in range(30):
+        n = int(rng.integers(2, 17))
+        m = int(rng.integers(0, 5))
+        me = min(m, max(0, n - 2))
+        if n > 13 and me >= 4:
+            m = 3
+        B = int(rng.integers(1, 700))
+        first = 64 * int(rng.integers(0, 1 << 20))
+        fmode = int(rng.integers(0, 3))
+        omode = int(rng.integers(0, 3))
+        f = int(rng.integers(0, n + 1))
+        seed = int(rng.integers(0, 1 << 62))
+        kw = dict(seed=seed, first_trial=first)
+        if fmode == 0:
+            kw["faulty"] = rng.integers(0, 1 << n, B, dtype=np.uint64).astype(np.uint32)
+        else:
+            kw.update(faulty_mode=fmode, f=f)
+        if omode == 0:
+            kw["order"] = rng.choice([0, 1, 2], B).astype(np.uint8)
+        else:
+            kw.update(order_mode=omode, order_value=int(rng.integers(0, 3)))
+        od, oo, ocnt = oracle_c.run(n, m, B, **kw)
+        res = engine.run(n, m, B, **kw)
+        tag = f"case {case}: n={n} m={m} B={B} fmode={fmode} omode={omode} f={f}"
+        same(res.decisions, od, "decisions " + tag)
+        same(res.outcome, oo, "outcome " + tag)
+        assert {k: res.counters[k] for k in ocnt} == ocnt, tag
