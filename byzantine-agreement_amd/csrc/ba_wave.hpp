@@ -207,15 +207,80 @@ __device__ __forceinline__ void wave_roots(const uint64_t* rc, uint64_t* au, uin
     }
 }
 
-// Per-trial epilogue (lane = trial) of W words, two words per iteration:
-// their LDS reads and logic interleave without the register blow-up (and
-// spills) of unrolling all W words at once.
+// Quorum epilogue of W words in two phases (ba.py:206-262, restated per trial
+// by trial_result in ba_device.hpp, which the oracle test pins):
+//  1. lane = word: the whole decision is bit-sliced over the word's 64 trials
+//     -- compile-time carry-save counts of attacks / non-retreats / faulty
+//     generals against the quorum thresholds, ORs and ANDs over the loyal
+//     lieutenants for agreement and validity -- and the run counters are
+//     popcounts of the resulting planes masked by the live-trial word.  The
+//     six outcome planes overwrite the word's faulty planes in LDS.
+//  2. lane = trial: the 2L decision bits and 6 outcome bits of each word are
+//     picked out of the 32-bit half holding this lane (one bfe + one shift-or
+//     per bit) and stored.
+// Per trial this is ~3x fewer instructions than running trial_result in every
+// lane, which needed all 2L+N+3 bits gathered first.
+template <int N, uint32_t ME>
+__device__ __forceinline__ void epilogue_planes(uint64_t* inw, const uint64_t* au,
+                                                TrialCounts& tc) {
+    constexpr int L = N - 1, NB = planes_c(N);
+    constexpr int needed = N == 1 ? 1 : (N <= 3 ? N - 1 : 2 * ((N - 1) / 3) + 1);
+    constexpr int K0 = L - needed;  // retreat: #(A|U) <= K0 (+1 when the commander retreats)
+    const uint64_t val = inw[N + 2], oo = inw[N + 1];
+    const uint64_t ob = inw[N] & ~oo, orr = ~inw[N] & ~oo;  // commander attack / retreat
+    const uint64_t f0 = inw[0];
+    Csa<NB> cA, cX, cF;
+    cF.template add<0>(f0);
+    uint64_t anyA = 0, anyU = 0, anyR = 0, allA = ~0ull, allR = ~0ull;
+    uint32_t nA = 0, nU = 0, nf = (uint32_t)__popcll(f0 & val);
+    static_for<0, L>([&](auto b) {
+        const uint64_t a = au[b()], u = au[L + b()] & ~a, x = a | u, f = inw[b() + 1];
+        cA.template add<b()>(a);
+        cX.template add<b()>(x);
+        cF.template add<b() + 1>(f);
+        anyA |= a & ~f;
+        anyU |= u & ~f;
+        anyR |= ~(x | f);
+        allA &= a | f;
+        allR &= ~x | f;
+        nA += (uint32_t)__popcll(a & val);
+        nU += (uint32_t)__popcll(u & val);
+        nf += (uint32_t)__popcll(f & val);
+    });
+    const uint64_t retreat = ~cX.template ge<L, K0 + 1>() | (orr & ~cX.template ge<L, K0 + 2>());
+    const uint64_t attc = cA.template ge<L, needed>() | (ob & cA.template ge<L, needed - 1>());
+    const uint64_t q1 = ~retreat & attc, q2 = ~retreat & ~attc;
+    const uint64_t agree = ~maj3(anyA, anyU, anyR);
+    const uint64_t appl = ~f0;
+    const uint64_t valid = appl & ((ob & allA) | (~ob & allR));
+    const uint64_t inb = (N > 3 * (int)ME) ? ~cF.template ge<N, (int)ME + 1>() : 0ull;
+    tc.v[C_TRIALS] += (uint32_t)__popcll(val);
+    tc.v[C_AGREE] += (uint32_t)__popcll(agree & val);
+    tc.v[C_VAPPL] += (uint32_t)__popcll(appl & val);
+    tc.v[C_VALID] += (uint32_t)__popcll(valid & val);
+    tc.v[C_QR] += (uint32_t)__popcll(retreat & val);
+    tc.v[C_QA] += (uint32_t)__popcll(q1 & val);
+    tc.v[C_QU] += (uint32_t)__popcll(q2 & val);
+    tc.v[C_UNDEF] += nU;
+    tc.v[C_INB] += (uint32_t)__popcll(inb & val);
+    tc.v[C_VIOL] += (uint32_t)__popcll(inb & (~agree | (appl & ~valid)) & val);
+    tc.v[C_FTOT] += nf;
+    tc.v[C_ATT] += nA;
+    inw[0] = q1;
+    inw[1] = q2;
+    inw[2] = agree;
+    inw[3] = appl;
+    inw[4] = valid;
+    inw[5] = inb;
+}
+
 template <int N, int W, uint32_t ME, int DIAG>
-__device__ __forceinline__ void wave_epilogue(const uint64_t* in0, const uint64_t* au0,
+__device__ __forceinline__ void wave_epilogue(uint64_t* in0, const uint64_t* au0,
                                               uint32_t lane, uint64_t w0, uint64_t batch,
                                               uint64_t* __restrict__ decisions,
                                               uint8_t* __restrict__ outcome, TrialCounts& tc) {
     constexpr int L = N - 1, NIN = N + 3;
+    static_assert(L <= 16, "decision word: 2 bits per lieutenant in the low 32 bits");
     if constexpr ((DIAG & 32) != 0) {  // lab: near-free stand-in epilogue
         static_for<0, W>([&](auto wq) {
             const uint64_t i = (w0 + wq()) * 64 + lane;
@@ -223,53 +288,29 @@ __device__ __forceinline__ void wave_epilogue(const uint64_t* in0, const uint64_
         });
         return;
     }
-    constexpr int EW = 2;
-#pragma unroll 1
-    for (int wb = 0; wb < W; wb += EW) {
-        uint64_t dec_out[EW];
-        uint32_t out_out[EW];
-        static_for<0, EW>([&](auto wq) {
-            const int w = wb + wq();
-            out_out[wq()] = 0xFFu;  // 0xFF: not a trial of this batch
-            dec_out[wq()] = 0;
-            if (W % EW != 0 && w >= W) return;
-            const uint64_t* inw = in0 + w * NIN;
-            const uint64_t* au = au0 + w * 2 * L;
-            const bool live = (inw[N + 2] >> lane) & 1ull;
-            uint32_t A = 0, U = 0, fm = 0;
-            static_for<0, L>([&](auto b) {
-                A |= (uint32_t)((au[b()] >> lane) & 1ull) << (b() + 1);
-                U |= (uint32_t)((au[L + b()] >> lane) & 1ull) << (b() + 1);
-            });
-            static_for<0, N>([&](auto g) { fm |= (uint32_t)((inw[g()] >> lane) & 1ull) << g(); });
-            const uint32_t ob = (uint32_t)(inw[N] >> lane) & 1u;
-            const uint32_t oo = (uint32_t)(inw[N + 1] >> lane) & 1u;
-            const TrialResult r = trial_result(N, ME, fm, oo ? 2u : ob, A, U);
-            const uint32_t lv = live ? 1u : 0u;
-            const uint32_t q = r.out & 3, agree = (r.out >> 2) & 1, appl = (r.out >> 3) & 1;
-            const uint32_t valid = (r.out >> 4) & 1, inb = (r.out >> 5) & 1;
-            tc.v[C_TRIALS] += lv;
-            tc.v[C_AGREE] += lv & agree;
-            tc.v[C_VAPPL] += lv & appl;
-            tc.v[C_VALID] += lv & valid;
-            tc.v[C_QR] += lv & (q == 0);
-            tc.v[C_QA] += lv & (q == 1);
-            tc.v[C_QU] += lv & (q == 2);
-            tc.v[C_UNDEF] += lv * r.nU;
-            tc.v[C_INB] += lv & inb;
-            tc.v[C_VIOL] += lv & inb & ((agree ^ 1u) | (appl & (valid ^ 1u)));
-            tc.v[C_FTOT] += lv * r.nf;
-            tc.v[C_ATT] += lv * r.nA;
-            dec_out[wq()] = r.dec;
-            out_out[wq()] = live ? r.out : 0xFFu;
+    for (uint32_t w = lane; w < (uint32_t)W; w += 64)
+        epilogue_planes<N, ME>(in0 + w * NIN, au0 + w * 2 * L, tc);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t half = lane >> 5, sh = lane & 31;
+    auto bit = [&](const uint64_t* p) -> uint32_t {
+        return __builtin_amdgcn_ubfe(reinterpret_cast<const uint32_t*>(p)[half], sh, 1);
+    };
+#pragma unroll 2
+    for (int w = 0; w < W; ++w) {
+        const uint64_t* inw = in0 + w * NIN;
+        const uint64_t* au = au0 + w * 2 * L;
+        const uint64_t i = (w0 + w) * 64 + lane;
+        const uint32_t live = bit(inw + N + 2);  // 0: not a trial of this batch
+        uint32_t dec = 0, out = 0;
+        static_for<0, L>([&](auto b) {
+            dec |= bit(au + b()) << (2 * b());
+            dec |= bit(au + L + b()) << (2 * b() + 1);
         });
-        static_for<0, EW>([&](auto wq) {
-            const uint64_t i = (w0 + wb + wq()) * 64 + lane;
-            if (out_out[wq()] != 0xFFu) {
-                if (!(DIAG & 1) && decisions) decisions[i] = dec_out[wq()];
-                if (!(DIAG & 2) && outcome) outcome[i] = (uint8_t)out_out[wq()];
-            }
-        });
+        static_for<0, 6>([&](auto k) { out |= bit(inw + k()) << k(); });
+        if (live) {
+            if (!(DIAG & 1) && decisions) decisions[i] = dec;
+            if (!(DIAG & 2) && outcome) outcome[i] = (uint8_t)out;
+        }
     }
 }
 
