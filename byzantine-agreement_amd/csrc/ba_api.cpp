@@ -141,7 +141,7 @@ void LevelsLayout::plan(const Geometry& g, uint64_t W_, bool leaf, uint32_t jb_,
     VAL = o; o += W;
     Lk.assign(g.me + 1, 0);
     for (uint32_t k = 0; k <= g.me; ++k) {
-        if (leaf && k == g.me) break;  // generated on the fly by k_leaf
+        if (leaf && k + 1 >= g.me) break;  // L_{me-1}, L_me generated on the fly by k_leaf
         Lk[k] = o;
         o += cnt[k] * W;
     }

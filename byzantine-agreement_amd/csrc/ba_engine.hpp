@@ -86,7 +86,7 @@ struct LevelsLayout {
     std::vector<uint64_t> Lk, Rp;  // Rp[p] valid for 1 <= p < me
     std::vector<uint64_t> base, cnt;
     uint64_t total = 0;
-    bool leaf_fused = false;       // L_me not materialised (k_leaf)
+    bool leaf_fused = false;       // L_{me-1}, L_me not materialised (k_leaf)
     void plan(const Geometry& g, uint64_t W, bool leaf, uint32_t jb, uint32_t je);
     static uint64_t words_per_trial_word(const Geometry& g, bool leaf, uint32_t jb, uint32_t je);
 };
@@ -123,8 +123,9 @@ bool wave_supported(const Geometry& g);
 hipError_t launch_wave_engine(const RunArgs& a, const Geometry& g);
 bool plan_fused(const Geometry& g, FusedPlan& fp);
 hipError_t launch_leaf(const Geometry& g, uint64_t seed, uint64_t gw0, uint32_t W,
-                       uint32_t srbase, uint32_t srcnt, const uint64_t* Lm1, const uint64_t* F,
-                       const uint64_t* d_members, uint64_t* Rm1, hipStream_t st, Prof* prof);
+                       uint32_t srbase, uint32_t srcnt, uint32_t lbase, const uint64_t* Lm2,
+                       const uint8_t* d_sender, const uint64_t* F, const uint64_t* d_members,
+                       uint64_t* Rm1, hipStream_t st, Prof* prof);
 hipError_t launch_fused(const RunArgs& a, const Geometry& g, bool plan_ok, const FusedPlan& fp,
                         const FusedPlan* d_fp, const uint8_t* d_sender, uint64_t* partials);
 

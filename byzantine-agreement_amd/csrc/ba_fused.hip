@@ -22,28 +22,45 @@ namespace ba {
 // ---------------------------------------------------------------------------
 // LEVELS: one thread per (leaf block, word)
 // ---------------------------------------------------------------------------
-// Leaf blocks sr = srbase + idx / W (a first-hop subtree range of level me-2);
-// L_{me-1} / R_{me-1} are indexed from the range's first block.
+// Leaf blocks sr = srbase + idx / W (a first-hop subtree range of level me-2).
+// Relay level me-1 is fused in: the S diagonal values of block sr all relay
+// its parent L_{me-2}[sr] through the same sender (the last general of sr,
+// snd2[sr]), so the thread reads one parent word and draws the level me-1
+// lies itself (the same Philox pairs k_relay would draw: keyed by global slot
+// pair, so the bits are identical).  L_{me-1} and L_me are never materialised.
+// L_{me-2} is indexed from lbase (its range's first slot; level 0 is whole),
+// R_{me-1} from the range's first block.
 template <int S>
 __global__ __launch_bounds__(256) void k_leaf(uint32_t me, uint64_t seed, uint64_t gw0,
                                               FastDiv divW, uint32_t work, uint32_t srbase,
-                                              const uint64_t* __restrict__ Lm1,
+                                              uint32_t lbase, const uint64_t* __restrict__ Lm2,
+                                              const uint8_t* __restrict__ snd2,
                                               const uint64_t* __restrict__ F,
                                               const uint64_t* __restrict__ members,
                                               uint64_t* __restrict__ Rm1) {
+    constexpr int NPD = (S + 1) / 2;  // level me-1 slot pairs a block's S slots touch
     const uint32_t W = divW.d;
     for (uint32_t idx = blockIdx.x * 256 + threadIdx.x; idx < work; idx += gridDim.x * 256) {
         const uint32_t sl = fdiv(idx, divW);
         const uint32_t w = idx - sl * W;
         const uint32_t sr = srbase + sl;
+        const uint64_t gw = gw0 + w;
         const uint64_t mem = members[sr];  // S member ids, 5 bits each
+        const uint64_t par = Lm2[(uint64_t)(sr - lbase) * W + w];
+        const uint64_t fs = F[(uint64_t)snd2[sr] * W + w];
+        const uint32_t x0 = sr * (uint32_t)S;  // first level me-1 slot of the block
+        uint64_t lw[2 * NPD];
+        lie_pairs<NPD>(seed, me - 1, x0 >> 1, gw, lw);
+        const uint64_t oddmask = 0ull - (uint64_t)(x0 & 1u);  // odd S only: block starts mid-pair
         uint64_t diag[S], Fm[S], R[S];
         static_for<0, S>([&](auto a) {
-            const uint64_t x = (uint64_t)sl * S + a();
-            diag[a()] = Lm1[x * W + w];
+            uint64_t lie;
+            if constexpr (S % 2 == 1) lie = lw[a()] ^ ((lw[a()] ^ lw[a() + 1]) & oddmask);
+            else lie = lw[a()];
+            diag[a()] = (fs & lie) | (~fs & par);
             Fm[a()] = F[((mem >> (5 * a())) & 31u) * W + w];
         });
-        leaf_block<S>(me, seed, gw0 + w, sr, diag, Fm, R);
+        leaf_block<S>(me, seed, gw, sr, diag, Fm, R);
         static_for<0, S>([&](auto b) { Rm1[((uint64_t)sl * S + b()) * W + w] = R[b()]; });
     }
 }
@@ -463,26 +480,28 @@ bool leaf_supported(const Geometry& g) {
 
 template <int S>
 static void launch_leaf_s(uint32_t me, uint64_t seed, uint64_t gw0, uint32_t W, uint32_t work,
-                          uint32_t srbase, const uint64_t* Lm1, const uint64_t* F,
-                          const uint64_t* snd, uint64_t* Rm1, hipStream_t st) {
+                          uint32_t srbase, uint32_t lbase, const uint64_t* Lm2,
+                          const uint8_t* snd2, const uint64_t* F, const uint64_t* mem,
+                          uint64_t* Rm1, hipStream_t st) {
     uint64_t b = (work + 255) / 256;
     if (b > 16384) b = 16384;
     if (b < 1) b = 1;
     hipLaunchKernelGGL(k_leaf<S>, dim3((uint32_t)b), dim3(256), 0, st, me, seed, gw0,
-                       make_fastdiv(W), work, srbase, Lm1, F, snd, Rm1);
+                       make_fastdiv(W), work, srbase, lbase, Lm2, snd2, F, mem, Rm1);
 }
 
 hipError_t launch_leaf(const Geometry& g, uint64_t seed, uint64_t gw0, uint32_t W,
-                       uint32_t srbase, uint32_t srcnt, const uint64_t* Lm1, const uint64_t* F,
-                       const uint64_t* d_members, uint64_t* Rm1, hipStream_t st, Prof* prof) {
+                       uint32_t srbase, uint32_t srcnt, uint32_t lbase, const uint64_t* Lm2,
+                       const uint8_t* d_sender, const uint64_t* F, const uint64_t* d_members,
+                       uint64_t* Rm1, hipStream_t st, Prof* prof) {
     ProfScope ps(prof, "k_leaf", st);
     const uint32_t S = g.n - g.me;
     const uint32_t work = (uint32_t)((uint64_t)srcnt * W);
     if (work == 0) return hipSuccess;
-    const uint64_t* snd = d_members;
+    const uint8_t* snd2 = d_sender + g.sender_off[g.me - 2];  // last general of each level me-2 slot
     switch (S) {
 #define LEAF_CASE(s) \
-    case s: launch_leaf_s<s>(g.me, seed, gw0, W, work, srbase, Lm1, F, snd, Rm1, st); break;
+    case s: launch_leaf_s<s>(g.me, seed, gw0, W, work, srbase, lbase, Lm2, snd2, F, d_members, Rm1, st); break;
         LEAF_CASE(2) LEAF_CASE(3) LEAF_CASE(4) LEAF_CASE(5) LEAF_CASE(6) LEAF_CASE(7)
         LEAF_CASE(8) LEAF_CASE(9) LEAF_CASE(10) LEAF_CASE(11) LEAF_CASE(12)
 #undef LEAF_CASE

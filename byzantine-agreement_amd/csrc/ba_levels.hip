@@ -13,6 +13,7 @@
 namespace ba {
 
 constexpr int kBlock = 256;
+constexpr uint32_t kLoadChunk = 8;  // child loads issued together by the majority kernels
 
 __device__ __forceinline__ uint32_t grid_threads() { return gridDim.x * kBlock; }
 
@@ -95,6 +96,86 @@ __global__ __launch_bounds__(kBlock) void k_relay(uint32_t k, uint32_t xbase, ui
 }
 
 // ---------------------------------------------------------------------------
+// relay levels 0..K in ONE launch (the levels above the leaf blocks are small:
+// for n=16, m=5 they are 15 + 210 + 2730 + 32760 slots, where four k_relay
+// launches cost more in launch gaps than in work).  Items [0, np0*W) write
+// level 0 (always whole).  The other items own one level-K slot pair of the
+// range and word: each walks its slots' ancestor chain from the commander down,
+// drawing the lie pair of every ancestor (keyed by global slot pair, as
+// k_relay), and writes its level-K slots plus every ancestor it is the first
+// descendant of (x == a * D[k]).  Redundant draws: K per level-K pair, ~4%
+// of a depth-5 tree's Philox calls.
+// ---------------------------------------------------------------------------
+constexpr int kTopMax = 6;
+struct TopPlan {
+    uint32_t K, L;                     // deepest level; lieutenants (= level-0 slots)
+    uint32_t np0;                      // level-0 slot pairs
+    uint32_t xbK, xeK;                 // level-K slot range [xbK, xeK)
+    uint32_t base[kTopMax + 1];        // first slot of level k's range (level 0: 0)
+    uint64_t off[kTopMax + 1];         // scratch offset of level k
+    uint32_t snd_off[kTopMax + 1];     // sender table offset of level k (k < K)
+    FastDiv D[kTopMax + 1];            // D[k] = prod_{i=k+1..K} (L - i): level-K slots per level-k slot
+};
+
+__global__ __launch_bounds__(kBlock) void k_relay_top(TopPlan tp, FastDiv divW, uint32_t work,
+                                                      uint64_t seed, uint64_t gw0,
+                                                      const uint8_t* __restrict__ sender,
+                                                      uint64_t* __restrict__ scratch,
+                                                      uint64_t offF, uint64_t offOB) {
+    const uint32_t W = divW.d;
+    const uint32_t work0 = tp.np0 * W;
+    const uint64_t* F = scratch + offF;
+    for (uint32_t idx = blockIdx.x * kBlock + threadIdx.x; idx < work; idx += grid_threads()) {
+        if (idx < work0) {  // level 0, whole: commander -> lieutenant x (ba.py:263-277)
+            const uint32_t p = fdiv(idx, divW), w = idx - p * W;
+            uint64_t lie[2];
+            lie_pair(seed, 0, p, gw0 + w, lie[0], lie[1]);
+            const uint64_t f0 = F[w], ob = scratch[offOB + w];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t x = 2 * p + h;
+                if (x < tp.L) scratch[tp.off[0] + (uint64_t)x * W + w] = (f0 & lie[h]) | (~f0 & ob);
+            }
+            continue;
+        }
+        const uint32_t it = idx - work0;
+        const uint32_t pl = fdiv(it, divW), w = it - pl * W;
+        const uint64_t gw = gw0 + w;
+        const uint32_t pairK = (tp.xbK >> 1) + pl;
+        uint64_t lieK[2];
+        lie_pair(seed, tp.K, pairK, gw, lieK[0], lieK[1]);
+        const uint64_t ob = scratch[offOB + w];
+        uint32_t prev_parent = 0xFFFFFFFFu;
+        uint64_t parent_val = 0;
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t x = 2 * pairK + h;
+            if (x < tp.xbK || x >= tp.xeK) continue;
+            const uint32_t par = fdiv(x, tp.D[tp.K - 1]);  // level K-1 ancestor
+            if (par != prev_parent) {  // walk the chain levels 0..K-1 (once per parent)
+                uint64_t v = ob;
+#pragma unroll
+                for (int k = 0; k < kTopMax; ++k) {
+                    if (k >= (int)tp.K) break;
+                    const uint32_t a = fdiv(x, tp.D[k]);
+                    const uint64_t fw = k == 0 ? F[w]
+                                               : F[(uint64_t)sender[tp.snd_off[k - 1] + fdiv(x, tp.D[k - 1])] * W + w];
+                    uint64_t l2[2];
+                    lie_pair(seed, (uint32_t)k, a >> 1, gw, l2[0], l2[1]);
+                    v = (fw & l2[a & 1u]) | (~fw & v);
+                    if (k >= 1 && x == a * tp.D[k].d)  // first descendant writes the ancestor
+                        scratch[tp.off[k] + (uint64_t)(a - tp.base[k]) * W + w] = v;
+                }
+                prev_parent = par;
+                parent_val = v;
+            }
+            const uint64_t fw = F[(uint64_t)sender[tp.snd_off[tp.K - 1] + par] * W + w];
+            scratch[tp.off[tp.K] + (uint64_t)(x - tp.base[tp.K]) * W + w] =
+                (fw & lieK[h]) | (~fw & parent_val);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // inner majority level p (1 <= p < me): one thread per (slot, word).  Level p
 // starts at global slot ybase, its child level at cbase (subtree ranges).
 // ---------------------------------------------------------------------------
@@ -115,10 +196,18 @@ __global__ __launch_bounds__(kBlock) void k_majority(uint32_t s, FastDiv divW, F
         Count<P> cnt;
         cnt.add(Lp[(uint64_t)yl * W + w]);
         const uint64_t base = (uint64_t)sr * s;
-        for (uint32_t a = 0; a < s; ++a) {
-            if (a == b) continue;
-            const uint64_t cs = (base + a) * (s - 1) + (b - (b > a)) - cbase;
-            cnt.add(C[cs * W + w]);
+        // children in chunks of kLoadChunk: every load of a chunk is in flight
+        // before the first add (a load-add loop waits one HBM latency per child)
+        for (uint32_t a0 = 0; a0 < s; a0 += kLoadChunk) {
+            uint64_t v[kLoadChunk];
+#pragma unroll
+            for (uint32_t q = 0; q < kLoadChunk; ++q) {
+                const uint32_t a = a0 + q;
+                const uint64_t cs = (base + a) * (s - 1) + (b - (b > a)) - cbase;
+                v[q] = (a < s && a != b) ? C[cs * W + w] : 0ull;
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < kLoadChunk; ++q) cnt.add(v[q]);  // absent children add 0
         }
         Rp[(uint64_t)yl * W + w] = cnt.ge(thr);
     }
@@ -151,10 +240,16 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(uint32_t n, uint32_t me, ui
             Count<P> cnt;
             cnt.add(scratch[offL0 + (uint64_t)b * W + w]);
             if (me >= 1) {
-                for (uint32_t a = 0; a < L; ++a) {
-                    if (a == b) continue;
-                    const uint64_t cs = (uint64_t)a * (L - 1) + (b - (b > a));
-                    cnt.add(C1[cs * W + w]);
+                for (uint32_t a0 = 0; a0 < L; a0 += kLoadChunk) {  // loads in flight together
+                    uint64_t v[kLoadChunk];
+#pragma unroll
+                    for (uint32_t q = 0; q < kLoadChunk; ++q) {
+                        const uint32_t a = a0 + q;
+                        const uint64_t cs = (uint64_t)a * (L - 1) + (b - (b > a));
+                        v[q] = (a < L && a != b) ? C1[cs * W + w] : 0ull;
+                    }
+#pragma unroll
+                    for (uint32_t q = 0; q < kLoadChunk; ++q) cnt.add(v[q]);
                 }
             }
             const uint32_t c = me >= 1 ? L : 1u;  // OM(0): the direct value alone
@@ -360,11 +455,42 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
         if (p == 1 && job.votes_out) return job.votes_out;
         return scratch + lay.Rp[p];
     };
-    // relay, top-down (levels 0..me, or 0..me-1 when the leaf level is fused
-    // into the leaf-parent majority and never materialised).  Level 0 is
-    // always whole; a root-only pass stops there.
-    const uint32_t ktop = !job.tree ? 0 : (lay.leaf_fused ? g.me - 1 : g.me);
-    for (uint32_t k = 0; k <= ktop; ++k) {
+    // relay, top-down (levels 0..me, or 0..me-2 when the two bottom levels
+    // are fused into the leaf-block kernel and never materialised).  Level 0
+    // is always whole; a root-only pass stops there.
+    const uint32_t ktop = !job.tree ? 0 : (lay.leaf_fused ? g.me - 2 : g.me);
+    // levels 0..kf in one k_relay_top launch; a materialised leaf level (no
+    // leaf fusion) stays a k_relay launch, since a chain walk per leaf pair
+    // would multiply the biggest level's draws.  BA_NO_TOP_RELAY=1: one
+    // k_relay launch per level (A/B and parity tests).
+    static const bool no_top = getenv("BA_NO_TOP_RELAY") && atoi(getenv("BA_NO_TOP_RELAY")) != 0;
+    const uint32_t kf = (lay.leaf_fused || !job.tree || g.me == 0) ? ktop : g.me - 1;
+    uint32_t k_first = 0;
+    if (!no_top && kf <= (uint32_t)kTopMax) {
+        TopPlan tp{};
+        tp.K = kf;
+        tp.L = g.L;
+        tp.np0 = (g.L + 1) / 2;
+        tp.xbK = (uint32_t)lay.base[kf];
+        tp.xeK = (uint32_t)(lay.base[kf] + lay.cnt[kf]);
+        for (uint32_t k = 0; k <= kf; ++k) {
+            tp.base[k] = (uint32_t)lay.base[k];
+            tp.off[k] = lay.Lk[k];
+            tp.snd_off[k] = k < g.me ? (uint32_t)g.sender_off[k] : 0u;
+            uint64_t d = 1;
+            for (uint32_t i = k + 1; i <= kf; ++i) d *= g.L - i;
+            tp.D[k] = make_fastdiv((uint32_t)d);
+        }
+        const uint32_t npK = kf == 0 ? 0u : (tp.xeK + 1) / 2 - tp.xbK / 2;
+        const uint32_t work = (uint32_t)((uint64_t)(tp.np0 + (tp.xeK > tp.xbK ? npK : 0u)) * W);
+        ProfScope ps(a.prof, "k_relay_top", st);
+        hipLaunchKernelGGL(k_relay_top, dim3(blocks_for(work, 16384)), dim3(kBlock), 0, st, tp,
+                           make_fastdiv((uint32_t)W), work, a.seed, gw0, d_sender, scratch, lay.F,
+                           lay.OB);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        k_first = kf + 1;
+    }
+    for (uint32_t k = k_first; k <= ktop; ++k) {
         const uint32_t xbase = (uint32_t)lay.base[k], xcnt = (uint32_t)lay.cnt[k];
         if (xcnt == 0) continue;
         const uint32_t npair = (xbase + xcnt + 1) / 2 - xbase / 2;
@@ -378,14 +504,15 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
                            a.seed, gw0, Lprev, Lptr(k), scratch + lay.F, snd);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    if (job.tree && lay.leaf_fused) {  // L_me generated on the fly: R_{me-1} straight from L_{me-1}
+    if (job.tree && lay.leaf_fused) {  // L_{me-1} and L_me on the fly: R_{me-1} from L_{me-2}
         // leaf blocks = slots of level me-2; level 0 is stored whole, but its
         // subtree range is the first-hop lieutenants [jb, je) themselves
         const bool top = g.me == 2;
         const uint32_t srbase = top ? lay.jb : (uint32_t)lay.base[g.me - 2];
         const uint32_t srcnt = top ? lay.je - lay.jb : (uint32_t)lay.cnt[g.me - 2];
-        e = launch_leaf(g, a.seed, gw0, (uint32_t)W, srbase, srcnt, Lptr(g.me - 1),
-                        scratch + lay.F, a.members, Rptr(g.me - 1), st, a.prof);
+        e = launch_leaf(g, a.seed, gw0, (uint32_t)W, srbase, srcnt, (uint32_t)lay.base[g.me - 2],
+                        Lptr(g.me - 2), d_sender, scratch + lay.F, a.members, Rptr(g.me - 1), st,
+                        a.prof);
         if (e != hipSuccess) return e;
     }
     // inner majorities, bottom-up (levels me-1..1, or me-2..1 after k_leaf)
