@@ -77,8 +77,10 @@ def kernel_bytes(name: str, n: int, m: int, batch: int) -> int:
         return 8 * words * (S[me] + S[me - 1])
     if name == "k_majority_leaf":  # read L_me + L_{me-1}, write R_{me-1}
         return 8 * words * (S[me] + 2 * S[me - 1])
-    if name == "k_leaf":  # leaf level never materialised: read L_{me-1}, write R_{me-1}
-        return 8 * words * 2 * S[me - 1]
+    if name == "k_leaf":  # levels me-1, me never materialised: read L_{me-2}, write R_{me-1}
+        return 8 * words * (S[me - 2] + S[me - 1])
+    if name == "k_relay_top":  # write levels 0..me-2 once
+        return 8 * words * sum(S[: me - 1])
     if name.startswith("k_fused") or name.startswith("k_om3w"):  # whole tree per launch
         return algorithmic_bytes_per_trial(n, m) * batch
     return 0

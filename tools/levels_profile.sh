@@ -3,10 +3,11 @@
 # original design) on the bench workload: rocprofv3 kernel stats plus PMC
 # HBM traffic per kernel, combined by tools/kernel_hbm.py into achieved GB/s
 # per kernel against the MI355X HBM peak.  Output: gpurun_out/levels${TAG}_*.
-# usage: [TAG=_n16m5 WL="--n 16 --m 5 --batch 1024"] tools/levels_profile.sh
+# usage: [TAG=_n16m5 WL="--n 16 --m 5 --batch 1024" CONFIG=16,5,1024,levels,k_leaf] tools/levels_profile.sh
 set -u
 TAG=${TAG:-}
 WL=${WL:-}
+CONFIG=${CONFIG:-10,3,1048576,levels,k_leaf}  # n,m,batch,engine,kernel (bench.py traffic lookup)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 mkdir -p gpurun_out/levels${TAG}_prof gpurun_out/levels${TAG}_pmc
@@ -18,7 +19,7 @@ for pass in "FETCH_SIZE" "WRITE_SIZE"; do
      -d "$ROOT/gpurun_out/levels${TAG}_pmc" -o "$pass" -- python3 $CMD > "$ROOT/gpurun_out/levels${TAG}_pmc_$pass.log" 2>&1) || exit $?
 done
 python3 tools/pmc_summary.py gpurun_out/levels${TAG}_pmc gpurun_out/levels${TAG}_pmc_summary.json \
-  --workload "bench.py --engine levels $WL" > gpurun_out/levels${TAG}_pmc_summary.log 2>&1
+  --workload "bench.py --engine levels $WL" --config "$CONFIG" > gpurun_out/levels${TAG}_pmc_summary.log 2>&1
 python3 tools/kernel_hbm.py gpurun_out/levels${TAG}_prof/run_kernel_stats.csv gpurun_out/levels${TAG}_pmc_summary.json \
   > gpurun_out/levels${TAG}_kernel_hbm.json
 cat gpurun_out/levels${TAG}_kernel_hbm.json
