@@ -151,10 +151,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # rehearsal knobs for a one-GPU box (never set by the driver): every rank on
+    # cuda:0 and gloo in place of RCCL, which refuses two ranks on one device
+    backend = os.environ.get("BA_BENCH_BACKEND", "nccl")
+    if os.environ.get("BA_BENCH_SHARE_GPU") == "1":
+        local = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local if world > 1 else 0)
