@@ -146,8 +146,12 @@ def test_oracle_votes_reproduce_root_decisions():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,m,B", [(10, 3, 200), (7, 1, 100), (9, 2, 130), (16, 5, 2)])
-def test_subtree_votes_match_oracle_gpu(engine, n, m, B):
+@pytest.mark.parametrize("n,m,B,nr", [(10, 3, 200, 4), (7, 1, 100, 4), (9, 2, 130, 4), (16, 5, 2, 4),
+                                      # odd n at depth 3: a first-hop subtree holds an odd
+                                      # number of level-1 slots, so with 3 ranks a range
+                                      # starts mid slot pair (k_relay_top's range edges)
+                                      (9, 3, 150, 3), (5, 3, 70, 3), (13, 3, 65, 5)])
+def test_subtree_votes_match_oracle_gpu(engine, n, m, B, nr):
     from ba_amd import dist as D
     from ba_amd import lib as L
     dev = torch.device("cuda", 0)
@@ -156,7 +160,7 @@ def test_subtree_votes_match_oracle_gpu(engine, n, m, B):
               first_trial=64 * 3)
     p = L.make_params(n, m, **{k: v for k, v in kw.items()})
     v_or = oracle_c.votes(n, m, B, **kw)
-    ranges = D.subtree_ranges(n - 1, 4)
+    ranges = D.subtree_ranges(n - 1, nr)
     parts = []
     for jb, je in ranges:
         if je > jb:
