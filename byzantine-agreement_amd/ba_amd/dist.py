@@ -130,3 +130,92 @@ def run_instance_split(backend, params: L.Params, batch: int, group=None):
         parts = [buf]
     full = torch.cat([parts[r][:(b - a) * (params.n - 2)] for r, (a, b) in enumerate(ranges)])
     return backend.root_from_votes(params, batch, full)
+
+
+class InstanceSplitGraphs:
+    """run_instance_split with the launch sequence captured in hipGraphs.
+
+    A config-5 call (n=16, m=5) is ~17 kernels, most of them small (input
+    bit-slicing, the fused top relay, three inner majority levels, the root
+    epilogue, the counter reduction), so at small batches the launch gaps cost
+    about as much as the work.  The local halves of the split are captured once
+    per (params, batch) and replayed: graph 1 = this rank's subtree votes into a
+    fixed buffer, graph 2 = root majorities + quorum over the gathered votes.
+    The all-gather between them (world > 1) stays an eager RCCL call, so the
+    graphs hold no collective.  Outputs are the same tensors on every replay
+    (overwritten); results equal run_instance_split's bit for bit (GPU test).
+    """
+
+    def __init__(self, engine: L.Engine, device: torch.device, params: L.Params, batch: int,
+                 group=None):
+        self.engine, self.device, self.params, self.batch, self.group = engine, device, params, batch, group
+        self.rank, self.world = _rank_world(group)
+        n = params.n
+        self.ranges = subtree_ranges(n - 1, self.world)
+        self.jb, self.je = self.ranges[self.rank]
+        W = (batch + 63) // 64
+        self.rows = [L.vote_slots(n, params.m, a, b) for a, b in self.ranges]
+        self.stream = torch.cuda.Stream(device)
+        self.buf = torch.zeros((max(self.rows), W), dtype=torch.int64, device=device)
+        self.full = (self.buf if self.world == 1 else
+                     torch.zeros((sum(self.rows), W), dtype=torch.int64, device=device))
+        self.gathered = (None if self.world == 1 else
+                         torch.zeros((self.world, max(self.rows), W), dtype=torch.int64, device=device))
+        self.dec = torch.empty(batch, dtype=torch.int64, device=device)
+        self.out = torch.empty(batch, dtype=torch.uint8, device=device)
+        self.cnt = torch.zeros(16, dtype=torch.int64, device=device)
+        with torch.cuda.stream(self.stream):  # warm-up: geometry upload, scratch growth
+            self._tree()
+            self._gather()
+            self._root()
+        torch.cuda.synchronize(device)
+        if self.world == 1:  # no collective: one graph for the whole call
+            self.g_tree = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_tree, stream=self.stream):
+                self._tree()
+                self._root()
+            self.g_root = None
+        else:
+            self.g_tree = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_tree, stream=self.stream):
+                self._tree()
+            self.g_root = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_root, stream=self.stream):
+                self._root()
+
+    def _tree(self):
+        if self.je > self.jb:
+            self.engine.subtree_votes_device(self.params, self.batch, self.jb, self.je,
+                                             self.buf.data_ptr(),
+                                             stream=self.stream.cuda_stream)
+
+    def _gather(self):
+        if self.world == 1:
+            return
+        dist.all_gather([self.gathered[r] for r in range(self.world)], self.buf, group=self.group)
+        o = 0
+        for r, k in enumerate(self.rows):
+            self.full[o:o + k].copy_(self.gathered[r, :k])
+            o += k
+
+    def _root(self):
+        self.cnt.zero_()
+        self.engine.root_from_votes_device(self.params, self.batch, self.full.data_ptr(),
+                                           self.cnt.data_ptr(), d_decisions=self.dec.data_ptr(),
+                                           d_outcome=self.out.data_ptr(),
+                                           stream=self.stream.cuda_stream)
+
+    def replay(self):
+        """One split call; returns (decisions, outcome, counters) (reused tensors).
+        Ordered after the caller's current stream and before its later work."""
+        if self.g_root is None:  # replays on the caller's current stream
+            self.g_tree.replay()
+            return self.dec, self.out, self.cnt
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            self.g_tree.replay()
+            self._gather()
+            self.g_root.replay()
+        cur.wait_stream(self.stream)
+        return self.dec, self.out, self.cnt

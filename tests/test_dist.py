@@ -211,3 +211,24 @@ def test_split_api_errors(engine):
     with pytest.raises(L.BAError) as ei:
         engine.subtree_votes_device(p0, 64, 0, 2, v.data_ptr())
     assert ei.value.code == L.ENOTSUP
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,m,B", [(16, 5, 300), (10, 3, 1000), (9, 3, 150)])
+def test_instance_split_graphs_equal_eager(engine, n, m, B):
+    """The hipGraph-captured split (InstanceSplitGraphs) replays to the same
+    decisions / outcome bytes / counters as eager run_instance_split, on every
+    replay (the counters are re-zeroed inside the graph)."""
+    from ba_amd import dist as D
+    from ba_amd import lib as L
+    dev = torch.device("cuda", 0)
+    p = L.make_params(n, m, seed=0xBA5EED, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3,
+                      order_mode=L.ORDER_RANDOM, first_trial=64 * 5)
+    ref_dec, ref_out, ref_cnt = D.run_instance_split(D.DeviceBackend(engine, dev), p, B)
+    g = D.InstanceSplitGraphs(engine, dev, p, B)
+    for _ in range(3):
+        dec, out, cnt = g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(dec, ref_dec)
+        assert torch.equal(out, ref_out)
+        assert torch.equal(cnt, ref_cnt)

@@ -105,10 +105,19 @@ def main():
                                                for _ in range(reps)][-1], world, dev)
             res[B] = {"seconds_per_call": dt / reps, "instances_per_s": B * reps / dt,
                       "counters": counters(cnt)}
+            # the same call replayed from hipGraphs (D.InstanceSplitGraphs)
+            g = D.InstanceSplitGraphs(eng, dev, p, B)
+            (gd, go, gc), gdt = timed(lambda: [g.replay() for _ in range(reps)][-1], world, dev)
+            if not (torch.equal(gd, dec) and torch.equal(go, o) and torch.equal(gc, cnt)):
+                raise SystemExit("config 5: graph replay differs from the eager split")
+            res[B]["graph_seconds_per_call"] = gdt / reps
+            res[B]["graph_instances_per_s"] = B * reps / gdt
         out.append({"config": 5, "workload": f"OM({m}) n={n} (3,999,675 tree slots), first-hop "
                     f"subtree split over {world} GPU(s), votes all-gathered",
                     "latency_one_instance_ms": res[1]["seconds_per_call"] * 1e3,
+                    "latency_one_instance_ms_graph": res[1]["graph_seconds_per_call"] * 1e3,
                     "batch": a.batch5, "throughput_instances_per_s": res[a.batch5]["instances_per_s"],
+                    "throughput_instances_per_s_graph": res[a.batch5]["graph_instances_per_s"],
                     "n_gpus": world, "counters_batch": res[a.batch5]["counters"]})
 
     if rank == 0:
