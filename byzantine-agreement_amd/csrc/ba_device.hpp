@@ -487,6 +487,30 @@ __device__ __forceinline__ void block_counts_out(const TrialCounts& tc, uint64_t
     }
 }
 
+// Block-reduce per-thread counts, then wave 0 adds the block's totals into
+// `counters` through the sink (one reporting unit per block; every block of
+// the launch must call it).  Replaces a partial-row write + k_reduce launch.
+template <int BLOCK>
+__device__ __forceinline__ void block_counts_sink(const TrialCounts& tc, uint64_t* counters,
+                                                  const Sink& sk) {
+    __shared__ uint64_t red[BLOCK / 64][C_NUM];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < C_NUM; ++i) {
+        uint64_t x = tc.v[i];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+        if (lane == 0) red[wv][i] = x;
+    }
+    __syncthreads();
+    if (wv == 0) {
+        uint64_t s = 0;
+        if (lane < (uint32_t)C_NUM)
+            for (int w = 0; w < BLOCK / 64; ++w) s += red[w][lane];
+        sink_counters(lane, s, blockIdx.x, gridDim.x, counters, sk);
+    }
+}
+
 // Synthetic inputs (docs/SEMANTICS.md §4): u[i] = word i%4 of
 // Philox(ctr = (i/4, 0xFFFFFFFF, t_lo, t_hi)).  The partial Fisher-Yates
 // permutation lives in a per-thread LDS row (dynamic indices).

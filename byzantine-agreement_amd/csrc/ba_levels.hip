@@ -225,7 +225,7 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(uint32_t n, uint32_t me, ui
                                                      const uint64_t* __restrict__ C1,
                                                      uint64_t* __restrict__ decisions,
                                                      uint8_t* __restrict__ outcome,
-                                                     uint64_t* __restrict__ partial) {
+                                                     uint64_t* __restrict__ counters, Sink sk) {
     __shared__ uint64_t sA[kBlock / 64][kMaxN], sU[kBlock / 64][kMaxN], sF[kBlock / 64][kMaxN];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t L = n - 1;
@@ -282,7 +282,7 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(uint32_t n, uint32_t me, ui
         }
         __syncthreads();
     }
-    block_counts_out<kBlock>(tc, partial);
+    block_counts_sink<kBlock>(tc, counters, sk);  // run counters: no k_reduce launch
 }
 
 // ---------------------------------------------------------------------------
@@ -429,7 +429,8 @@ static void launch_epilogue_p(uint32_t blocks, const RunArgs& a, uint64_t W, uin
                               uint64_t* dec, uint8_t* out, uint64_t* partials) {
     hipLaunchKernelGGL(k_epilogue<P>, dim3(blocks), dim3(kBlock), 0, a.stream, a.n, a.me, W, nt,
                        scratch, lay.F, lay.OB, lay.OO, lay.VAL, lay.Lk[0], C1, dec, out,
-                       partials);
+                       a.counters, a.sink);
+    (void)partials;
 }
 
 hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_t* d_sender,
@@ -548,8 +549,7 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
         case 4: launch_epilogue_p<4>(blocks, a, W, ntrials, scratch, lay, C1, dec, out, partials); break;
         default: launch_epilogue_p<5>(blocks, a, W, ntrials, scratch, lay, C1, dec, out, partials); break;
     } }
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    return launch_reduce(partials, (int)blocks, a.counters, st, a.prof);
+    return hipGetLastError();
 }
 
 }  // namespace ba
