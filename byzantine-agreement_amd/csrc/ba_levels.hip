@@ -96,6 +96,153 @@ __global__ __launch_bounds__(kBlock) void k_relay(uint32_t k, uint32_t xbase, ui
 }
 
 // ---------------------------------------------------------------------------
+// Bit-sliced root + quorum epilogue (4 <= n <= 16, me >= 1): a block owns 64
+// consecutive trial words, and the quorum is decided for all 64 trials of a
+// word at once with bit-plane counters (lane = word), as the WAVE engines'
+// epilogue does; trial_result (ba_device.hpp, the per-trial restatement of
+// ba.py:197-255 the oracle pins) is the reference it must equal.
+//   1. wave v computes the root majorities of receivers b = v, v+4, ...
+//      for the 64 words (lane = word: coalesced loads) into LDS A/U planes
+//   2. wave 0 (lane = word): quorum, IC1/IC2 and bound flags from the planes,
+//      run counters by popcount; six outcome planes + the live mask to LDS
+//   3. wave v extracts words v, v+4, ... per trial (lane = trial) and stores
+//      the decision word and outcome byte
+// LDS: [2L + 7 + n][64] uint64 (A planes, U planes, 6 outcome planes, live
+// mask, faulty planes).  Used from 64 words per launch up (one block per 64
+// words; below that the per-trial k_epilogue has more parallelism).
+// ---------------------------------------------------------------------------
+template <int P>
+__global__ __launch_bounds__(kBlock) void k_epilogue_bs(uint32_t n, uint32_t me, uint64_t W,
+                                                        const uint64_t* __restrict__ scratch,
+                                                        uint64_t offF, uint64_t offOB,
+                                                        uint64_t offOO, uint64_t offVAL,
+                                                        uint64_t offL0,
+                                                        const uint64_t* __restrict__ C1,
+                                                        uint64_t* __restrict__ decisions,
+                                                        uint8_t* __restrict__ outcome,
+                                                        uint64_t* __restrict__ counters, Sink sk) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t sp[];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t L = n - 1;
+    const uint32_t needed = 2 * ((n - 1) / 3) + 1;  // quorum of n >= 4 live generals
+    const uint32_t K0 = L - needed;                 // retreat: #(A|U) <= K0 (+1 if the order is retreat)
+    uint64_t* sOut = sp + 2 * L * 64;               // q1 q2 agree appl valid inb live
+    uint64_t* sF = sOut + 7 * 64;                   // faulty planes of the n generals
+    TrialCounts tc;
+    const uint64_t groups = (W + 63) / 64;
+    for (uint64_t gi = blockIdx.x; gi < groups; gi += gridDim.x) {
+        const uint64_t w = gi * 64 + lane;
+        const bool wok = w < W;
+        // 1. faulty planes to LDS (rows g = v, v+4, ...), then the root
+        //    majorities (L inputs: L_0[b] and the level-1 votes about b); every
+        //    load of a chunk is in flight before the first add
+        for (uint32_t g = wv; g < n; g += kBlock / 64)
+            sF[g * 64 + lane] = wok ? scratch[offF + (uint64_t)g * W + w] : 0ull;
+        for (uint32_t b = wv; b < L; b += kBlock / 64) {
+            Count<P> c;
+            if (wok) {
+                for (uint32_t a0 = 0; a0 < L; a0 += kLoadChunk) {  // a == b: the direct value L_0[b]
+                    uint64_t v[kLoadChunk];
+#pragma unroll
+                    for (uint32_t q = 0; q < kLoadChunk; ++q) {
+                        const uint32_t a = a0 + q;
+                        const uint64_t cs = (uint64_t)a * (L - 1) + (b - (b > a));
+                        v[q] = a >= L ? 0ull
+                                      : (a == b ? scratch[offL0 + (uint64_t)b * W + w] : C1[cs * W + w]);
+                    }
+#pragma unroll
+                    for (uint32_t q = 0; q < kLoadChunk; ++q) c.add(v[q]);
+                }
+            }
+            const uint64_t att = c.ge(L / 2 + 1);                        // strict majority
+            const uint64_t tie = (L & 1u) ? 0ull : (c.ge(L / 2) & ~att);  // root tie: undefined
+            sp[b * 64 + lane] = att;
+            sp[(L + b) * 64 + lane] = tie;
+        }
+        __syncthreads();
+        // 2. quorum and flags, lane = word
+        if (wv == 0) {
+            uint64_t val = 0, obr = 0, oo = 0;
+            if (wok) {
+                val = scratch[offVAL + w];
+                obr = scratch[offOB + w];
+                oo = scratch[offOO + w];
+            }
+            const uint64_t f0 = sF[lane];
+            const uint64_t ob = obr & ~oo, orr = ~obr & ~oo;  // commander attack / retreat
+            Count<P> cA, cX, cF;
+            cF.add(f0);
+            uint64_t anyA = 0, anyU = 0, anyR = 0, allA = ~0ull, allR = ~0ull;
+            uint32_t nA = 0, nU = 0, nf = (uint32_t)__popcll(f0 & val);
+            for (uint32_t b = 0; b < L; ++b) {
+                const uint64_t a = sp[b * 64 + lane], u = sp[(L + b) * 64 + lane], x = a | u;
+                const uint64_t f = sF[(b + 1) * 64 + lane];
+                cA.add(a);
+                cX.add(x);
+                cF.add(f);
+                anyA |= a & ~f;
+                anyU |= u & ~f;
+                anyR |= ~(x | f);
+                allA &= a | f;
+                allR &= ~x | f;
+                nA += (uint32_t)__popcll(a & val);
+                nU += (uint32_t)__popcll(u & val);
+                nf += (uint32_t)__popcll(f & val);
+            }
+            const uint64_t retreat = ~cX.ge(K0 + 1) | (orr & ~cX.ge(K0 + 2));
+            const uint64_t attc = cA.ge(needed) | (ob & cA.ge(needed - 1));
+            const uint64_t q1 = ~retreat & attc, q2 = ~retreat & ~attc;
+            const uint64_t agree = ~maj3(anyA, anyU, anyR);  // loyal lieutenants: one decision kind
+            const uint64_t appl = ~f0;
+            const uint64_t valid = appl & ((ob & allA) | (~ob & allR));
+            const uint64_t inb = n > 3 * me ? ~cF.ge(me + 1) : 0ull;
+            tc.v[C_TRIALS] += (uint32_t)__popcll(val);
+            tc.v[C_AGREE] += (uint32_t)__popcll(agree & val);
+            tc.v[C_VAPPL] += (uint32_t)__popcll(appl & val);
+            tc.v[C_VALID] += (uint32_t)__popcll(valid & val);
+            tc.v[C_QR] += (uint32_t)__popcll(retreat & val);
+            tc.v[C_QA] += (uint32_t)__popcll(q1 & val);
+            tc.v[C_QU] += (uint32_t)__popcll(q2 & val);
+            tc.v[C_UNDEF] += nU;
+            tc.v[C_INB] += (uint32_t)__popcll(inb & val);
+            tc.v[C_VIOL] += (uint32_t)__popcll(inb & (~agree | (appl & ~valid)) & val);
+            tc.v[C_FTOT] += nf;
+            tc.v[C_ATT] += nA;
+            sOut[0 * 64 + lane] = q1;
+            sOut[1 * 64 + lane] = q2;
+            sOut[2 * 64 + lane] = agree;
+            sOut[3 * 64 + lane] = appl;
+            sOut[4 * 64 + lane] = valid;
+            sOut[5 * 64 + lane] = inb;
+            sOut[6 * 64 + lane] = val;
+        }
+        __syncthreads();
+        // 3. per-trial decision words and outcome bytes, lane = trial
+        const uint32_t half = lane >> 5, sh = lane & 31;
+        auto bit = [&](const uint64_t* q) -> uint32_t {
+            return __builtin_amdgcn_ubfe(reinterpret_cast<const uint32_t*>(q)[half], sh, 1);
+        };
+        const uint32_t nw = (uint32_t)(W - gi * 64 < 64 ? W - gi * 64 : 64);
+        for (uint32_t j = wv; j < nw; j += kBlock / 64) {
+            if (!bit(sOut + 6 * 64 + j)) continue;  // not a trial of this batch
+            uint64_t dec = 0;
+            for (uint32_t b = 0; b < L; ++b) {
+                dec |= (uint64_t)bit(sp + b * 64 + j) << (2 * b);
+                dec |= (uint64_t)bit(sp + (L + b) * 64 + j) << (2 * b + 1);
+            }
+            uint32_t out = 0;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) out |= bit(sOut + k * 64 + j) << k;
+            const uint64_t i = (gi * 64 + j) * 64 + lane;
+            if (decisions) decisions[i] = dec;
+            if (outcome) outcome[i] = (uint8_t)out;
+        }
+        __syncthreads();
+    }
+    block_counts_sink<kBlock>(tc, counters, sk);
+}
+
+// ---------------------------------------------------------------------------
 // relay levels 0..K in ONE launch (the levels above the leaf blocks are small:
 // for n=16, m=5 they are 15 + 210 + 2730 + 32760 slots, where four k_relay
 // launches cost more in launch gaps than in work).  Items [0, np0*W) write
@@ -541,6 +688,22 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
     const uint32_t blocks = blocks_for(W * 64, kPartialRows);
     uint64_t* dec = a.decisions ? a.decisions + trial0 : nullptr;
     uint8_t* out = a.outcome ? a.outcome + trial0 : nullptr;
+    static const bool old_epi = getenv("BA_EPILOGUE_PER_TRIAL") && atoi(getenv("BA_EPILOGUE_PER_TRIAL")) != 0;
+    const uint64_t groups = (W + 63) / 64;
+    if (!old_epi && g.n >= 4 && g.n <= 16 && g.me >= 1 && groups >= 64) {  // bit-sliced epilogue
+        const uint32_t eb = (uint32_t)(groups < 4096 ? groups : 4096);
+        const size_t lds = (size_t)(2 * g.L + 7 + g.n) * 64 * 8;
+        ProfScope ps(a.prof, "k_epilogue", st);
+        if (planes_for(g.n) <= 4)
+            hipLaunchKernelGGL(k_epilogue_bs<4>, dim3(eb), dim3(kBlock), lds, st, a.n, a.me, W,
+                               scratch, lay.F, lay.OB, lay.OO, lay.VAL, lay.Lk[0], C1, dec, out,
+                               a.counters, a.sink);
+        else
+            hipLaunchKernelGGL(k_epilogue_bs<5>, dim3(eb), dim3(kBlock), lds, st, a.n, a.me, W,
+                               scratch, lay.F, lay.OB, lay.OO, lay.VAL, lay.Lk[0], C1, dec, out,
+                               a.counters, a.sink);
+        return hipGetLastError();
+    }
     { ProfScope ps(a.prof, "k_epilogue", st);
     switch (planes_for(g.L)) {
         case 1: launch_epilogue_p<1>(blocks, a, W, ntrials, scratch, lay, C1, dec, out, partials); break;
