@@ -35,7 +35,9 @@ EXPORTS = ["ba_version", "ba_device_count", "ba_ctx_create", "ba_ctx_destroy", "
            "ba_run_trials", "ba_run_trials_device", "ba_tree_slots", "ba_level_slots",
            "ba_engine_for", "ba_profile_enable", "ba_profile_read", "ba_mt_seed", "ba_mt_next32",
            "ba_om1_coin_count", "ba_mt_draw_coins", "ba_mt_table", "ba_vote_slots",
-           "ba_subtree_votes_device", "ba_root_from_votes_device", "ba_gen_inputs_device"]
+           "ba_subtree_votes_device", "ba_root_from_votes_device", "ba_gen_inputs_device",
+           "ba_ctx_device", "ba_comm_unique_id", "ba_comm_create", "ba_comm_destroy",
+           "ba_trial_share", "ba_run_trials_multi"]
 
 
 class BAError(RuntimeError):
@@ -118,6 +120,15 @@ def load(path: str | None = None):
                                             vp]
     lib.ba_root_from_votes_device.argtypes = [vp, ctypes.POINTER(Params), u64, vp, vp, vp, vp, vp,
                                               vp, vp]
+    lib.ba_ctx_device.argtypes = [vp, ctypes.POINTER(i32)]
+    lib.ba_comm_unique_id.argtypes = [ctypes.c_char_p]
+    lib.ba_comm_create.argtypes = [vp, i32, i32, ctypes.c_char_p, ctypes.POINTER(vp)]
+    lib.ba_comm_destroy.argtypes = [vp]
+    lib.ba_comm_destroy.restype = None
+    lib.ba_trial_share.argtypes = [u64, i32, i32, ctypes.POINTER(u64), ctypes.POINTER(u64)]
+    lib.ba_run_trials_multi.argtypes = [vp, vp, ctypes.POINTER(Params), u64, vp, vp,
+                                        ctypes.POINTER(Counters), ctypes.POINTER(u64),
+                                        ctypes.POINTER(u64)]
     if lib.ba_version() != ABI_VERSION:
         raise RuntimeError(f"libba_hip ABI {lib.ba_version()} != {ABI_VERSION}")
     if path is None:
@@ -256,6 +267,55 @@ class Engine:
         _check(self.lib, self.lib.ba_root_from_votes_device(
             self.handle, ctypes.byref(params), batch, d_faulty or None, d_order or None, d_votes,
             d_decisions or None, d_outcome or None, d_counters, stream or None))
+
+
+def comm_unique_id() -> bytes:
+    """RCCL unique id (BA_COMM_ID_BYTES) for ba_comm_create; rank 0 makes it."""
+    lib = load()
+    buf = ctypes.create_string_buffer(128)
+    _check(lib, lib.ba_comm_unique_id(buf))
+    return buf.raw
+
+
+def trial_share(total_trials: int, nranks: int, rank: int):
+    """(first, count) of rank's word-aligned share (ba_trial_share)."""
+    lib = load()
+    f, c = ctypes.c_uint64(), ctypes.c_uint64()
+    _check(lib, lib.ba_trial_share(total_trials, nranks, rank, ctypes.byref(f), ctypes.byref(c)))
+    return f.value, c.value
+
+
+class Comm:
+    """An RCCL communicator owned by the C ABI (ba_comm_create) on an Engine's
+    device: ba_run_trials_multi shards trials over the ranks and all-reduces
+    the run counters itself, for hosts without torch.distributed."""
+
+    def __init__(self, engine: Engine, nranks: int, rank: int, uid: bytes):
+        self.engine, self.lib = engine, engine.lib
+        h = ctypes.c_void_p()
+        _check(self.lib, self.lib.ba_comm_create(engine.handle, nranks, rank, uid, ctypes.byref(h)))
+        self.handle = h
+
+    def run_trials(self, params: Params, total_trials: int, d_decisions=0, d_outcome=0):
+        """-> (whole-job counters dict, share first, share count)."""
+        cnt = Counters()
+        f, c = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(self.lib, self.lib.ba_run_trials_multi(
+            self.engine.handle, self.handle, ctypes.byref(params), total_trials,
+            d_decisions or None, d_outcome or None, ctypes.byref(cnt), ctypes.byref(f),
+            ctypes.byref(c)))
+        return dict(zip(COUNTER_NAMES, [int(x) for x in cnt.v])), f.value, c.value
+
+    def close(self):
+        if self.handle:
+            self.lib.ba_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class MT:

@@ -30,6 +30,9 @@ static int fail(int code, const char* fmt, ...) {
     return code;
 }
 
+// ba_multi.cpp reports its errors through the same thread-local message
+extern "C" int ba_fail_internal(int code, const char* msg) { return fail(code, "%s", msg); }
+
 #define HIP_TRY(expr)                                                                 \
     do {                                                                              \
         hipError_t _e = (expr);                                                       \
@@ -317,6 +320,12 @@ extern "C" int ba_ctx_create(int device, ba_ctx** out) {
         return fail(BA_ENOMEM, "counter sink allocation failed");
     }
     *out = ctx;
+    return BA_OK;
+}
+
+extern "C" int ba_ctx_device(ba_ctx* ctx, int* device) {
+    if (!ctx || !device) return fail(BA_EINVAL, "ctx and device are required");
+    *device = ctx->device;
     return BA_OK;
 }
 

@@ -200,6 +200,35 @@ int ba_root_from_votes_device(struct ba_ctx* ctx, const ba_params* p, uint64_t b
                               const uint64_t* d_votes, uint64_t* d_decisions, uint8_t* d_outcome,
                               uint64_t* d_counters, void* stream);
 
+/* ---- multi-GPU trial data-parallel runs (no ba.py analogue:
+ * its generals are threads of one process) ---------------------------------
+ * One process per GPU.  Rank 0 calls ba_comm_unique_id and ships the
+ * BA_COMM_ID_BYTES bytes to every rank out of band (MPI, a socket, a file);
+ * every rank calls ba_comm_create on its ctx (which owns the RCCL communicator,
+ * a counter buffer and a stream).  ba_run_trials_multi resolves this rank's
+ * contiguous, 64-trial-word-aligned share (ba_trial_share) of the trials
+ * [p->first_trial, p->first_trial + total_trials) -- inputs drawn on the device
+ * (faulty/order modes other than GIVEN), Philox lies, every draw keyed by the
+ * global trial index -- writes this share's decisions / outcome bytes to the
+ * optional device buffers (share_count entries), and all-reduces the run
+ * counters over RCCL: counters_out holds the whole job's totals on every rank,
+ * equal to one unsharded ba_run_trials.  Blocking (returns after the
+ * all-reduce).  RCCL is opened at run time (librccl.so.1, or the copy already
+ * loaded in the process). */
+#define BA_COMM_ID_BYTES 128
+struct ba_comm;
+int ba_ctx_device(struct ba_ctx* ctx, int* device);
+int ba_comm_unique_id(unsigned char id[BA_COMM_ID_BYTES]);
+int ba_comm_create(struct ba_ctx* ctx, int nranks, int rank,
+                   const unsigned char id[BA_COMM_ID_BYTES], struct ba_comm** out);
+void ba_comm_destroy(struct ba_comm* comm);
+int ba_trial_share(uint64_t total_trials, int nranks, int rank, uint64_t* first,
+                   uint64_t* count);
+int ba_run_trials_multi(struct ba_ctx* ctx, struct ba_comm* comm, const ba_params* p,
+                        uint64_t total_trials, uint64_t* d_decisions, uint8_t* d_outcome,
+                        ba_counters* counters_out, uint64_t* share_first,
+                        uint64_t* share_count);
+
 /* Per-kernel timing (tracing aux subsystem; replaces nothing in ba.py, which
  * only prints).  When enabled, every kernel the ctx launches is bracketed by
  * HIP events on its launch stream; ba_profile_read syncs those events and

@@ -449,3 +449,32 @@ def test_levels_bitsliced_epilogue_vs_oracle(engine, n, m):
     same(res.decisions, od, f"decisions n={n} m={m}")
     same(res.outcome, oo, f"outcome n={n} m={m}")
     assert {k: res.counters[k] for k in ocnt} == ocnt
+
+
+def test_run_trials_multi_world1_rccl(engine):
+    """ba_run_trials_multi over a one-rank RCCL communicator owned by the C ABI:
+    the all-reduced counters equal one ba_run_trials_device call, and the
+    share's decisions equal the oracle's (world-N sharding is the same code
+    path with a different ba_trial_share; N>1 runs on the driver's node)."""
+    import torch
+    from ba_amd import lib as L
+    uid = L.comm_unique_id()
+    comm = L.Comm(engine, 1, 0, uid)
+    try:
+        n, m, B = 10, 3, 64 * 50 + 9
+        p = L.make_params(n, m, 0xBA5EED, L.LIE_PHILOX, L.FAULTY_RANDOM, 3, L.ORDER_RANDOM,
+                          L.ATTACK, L.ENGINE_AUTO, 64 * 7)
+        dec = torch.empty(B, dtype=torch.int64, device="cuda")
+        out = torch.empty(B, dtype=torch.uint8, device="cuda")
+        cnt, first, count = comm.run_trials(p, B, dec.data_ptr(), out.data_ptr())
+        assert (first, count) == (0, B)
+        od, oo, oc = oracle_c.run(n, m, B, seed=0xBA5EED, faulty_mode=L.FAULTY_RANDOM, f=3,
+                                  order_mode=L.ORDER_RANDOM, first_trial=64 * 7)
+        same(dec.cpu().numpy().view(np.uint64), od, "decisions")
+        same(out.cpu().numpy(), oo, "outcome")
+        assert {k: cnt[k] for k in oc} == oc
+        with pytest.raises(L.BAError) as ei:  # given inputs are not sharded by this entry
+            comm.run_trials(L.make_params(n, m, 1), B)
+        assert ei.value.code == L.EINVAL
+    finally:
+        comm.close()

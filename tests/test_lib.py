@@ -74,3 +74,20 @@ def test_carry_save_counter_host_check(tmp_path):
     subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-o", str(exe), src], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
+
+
+def test_trial_share_partitions():
+    """ba_trial_share: contiguous word-aligned shares covering every trial once."""
+    from ba_amd import lib as L
+    for total in (0, 1, 63, 64, 65, 1000, 1 << 20):
+        for world in (1, 2, 3, 8):
+            got = [L.trial_share(total, world, r) for r in range(world)]
+            pos = 0
+            for first, count in got:
+                assert first % 64 == 0
+                if count:
+                    assert first == pos
+                    pos = first + count
+            assert pos == total
+    with pytest.raises(L.BAError):
+        L.trial_share(10, 2, 2)
