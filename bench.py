@@ -137,7 +137,7 @@ def main():
     ap.add_argument("--fmax", type=int, default=-1)
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0xBA5EED)
     ap.add_argument("--engine", default="auto", choices=["auto", "fused", "levels"])
-    ap.add_argument("--cpu-budget-s", type=float, default=12.0)
+    ap.add_argument("--cpu-budget-s", type=float, default=16.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--inputs-in-kernel", action="store_true",
