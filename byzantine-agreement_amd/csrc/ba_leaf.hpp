@@ -25,7 +25,11 @@ __device__ __forceinline__ void static_for(F&& f) {
 // counters see a compile-time input schedule (Csa, ba_device.hpp).
 // The S(S-1)/2 Philox calls run in interleaved groups of PG (philox10_n);
 // each group's 2*PG lie words feed the counters before the next group starts.
+#ifdef BA_LEAF_PG  // lab builds: force the group size where it divides the pair count
+constexpr int leaf_philox_group(int npair) { return npair % BA_LEAF_PG == 0 ? BA_LEAF_PG : (npair % 3 == 0 ? 3 : (npair % 4 == 0 ? 4 : (npair % 2 == 0 ? 2 : 3))); }
+#else
 constexpr int leaf_philox_group(int npair) { return npair % 3 == 0 ? 3 : (npair % 4 == 0 ? 4 : (npair % 2 == 0 ? 2 : 3)); }
+#endif
 
 template <int S>
 __device__ __forceinline__ void leaf_block(uint32_t me, uint64_t seed, uint64_t gw, uint32_t sr,
