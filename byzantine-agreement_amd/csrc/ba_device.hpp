@@ -78,8 +78,20 @@ __host__ __device__ __forceinline__ void philox_mul2(uint32_t x, uint32_t z, uin
                                                      uint64_t& p1) {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(BA_PHILOX_C)
     if constexpr (I >= 2) {
+#ifdef BA_MAD_SPLIT_ASM
         p0 = mad_u64_u32_pinned(x, 0xD2511F53u);
         p1 = mad_u64_u32_pinned(z, 0xCD9E8D57u);
+#else
+        // Both products in one asm statement: the hazard recognizer puts one
+        // conservative s_nop after every inline-asm VALU def (it cannot see that
+        // a v_mad_u64_u32 is neither a trans op nor an op_sel/SDWA write), so a
+        // pair per statement halves them.  p0 is early-clobber: it is written
+        // before z is read.
+        uint64_t cc;
+        asm("v_mad_u64_u32 %0, %2, %3, %5, 0\n\tv_mad_u64_u32 %1, %2, %4, %6, 0"
+            : "=&v"(p0), "=v"(p1), "=&s"(cc)
+            : "v"(x), "v"(z), "s"(0xD2511F53u), "s"(0xCD9E8D57u));
+#endif
         return;
     }
 #endif
