@@ -19,8 +19,8 @@ _lib = None
 def load():
     global _lib
     if _lib is None:
-        src = os.path.join(ROOT, "oracle", "ba_oracle.c")
-        if not os.path.exists(SO) or os.path.getmtime(src) > os.path.getmtime(SO):
+        srcs = [os.path.join(ROOT, "oracle", f) for f in ("ba_oracle.c", "ba_sliced.c")]
+        if not os.path.exists(SO) or max(map(os.path.getmtime, srcs)) > os.path.getmtime(SO):
             subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
         lib = ctypes.CDLL(SO)
         u32, u64, vp = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p
@@ -32,6 +32,9 @@ def load():
         lib.ba_oracle_gen.argtypes = [u32, u64, u32, u32, u32, u32, u64, vp, vp]
         lib.ba_oracle_votes.argtypes = [u32, u32, u64, u32, u32, u32, u32, u64, u64, vp, vp, vp,
                                         ctypes.c_int]
+        lib.ba_sliced_run.argtypes = [u32, u32, u64, u32, u32, u32, u32, u64, u64, vp, vp, vp, vp,
+                                      vp, ctypes.c_int]
+        lib.ba_sliced_gen.argtypes = [u32, u64, u32, u32, u32, u32, u64, u64, vp, vp, ctypes.c_int]
         _lib = lib
     return _lib
 
@@ -87,3 +90,33 @@ def pack_votes(v, jb=0, je=None):
     bits = pad.reshape(W, 64, -1).transpose(2, 0, 1)  # slot, word, lane
     weights = (np.uint64(1) << np.arange(64, dtype=np.uint64))
     return (bits.astype(np.uint64) * weights).sum(axis=2, dtype=np.uint64)
+
+
+def sliced_run(n, m, batch, seed=0, faulty_mode=0, f=0, order_mode=0, order_value=1,
+               first_trial=0, faulty=None, order=None, threads=0, want_outputs=True):
+    """Word-sliced OpenMP port (oracle/ba_sliced.c), Philox lies only.
+    Returns (decisions, outcome, counters) like run(); outputs None when not wanted."""
+    lib = load()
+    faulty = None if faulty is None else np.ascontiguousarray(faulty, np.uint32)
+    order = None if order is None else np.ascontiguousarray(order, np.uint8)
+    dec = np.zeros(batch, np.uint64) if want_outputs else None
+    out = np.zeros(batch, np.uint8) if want_outputs else None
+    cnt = np.zeros(16, np.uint64)
+    rc = lib.ba_sliced_run(n, m, seed, faulty_mode, f, order_mode, order_value, first_trial, batch,
+                           _p(faulty), _p(order), _p(dec), _p(out), _p(cnt), threads)
+    if rc != 0:
+        raise RuntimeError(f"sliced port rc={rc}")
+    return dec, out, dict(zip(COUNTER_NAMES, [int(x) for x in cnt[:12]]))
+
+
+def sliced_gen(n, batch, seed=0, faulty_mode=1, f=0, order_mode=1, order_value=1, first_trial=0,
+               threads=0):
+    """Synthetic inputs (faulty uint32[batch], order uint8[batch]) of the given stream."""
+    lib = load()
+    faulty = np.zeros(batch, np.uint32)
+    order = np.zeros(batch, np.uint8)
+    rc = lib.ba_sliced_gen(n, seed, faulty_mode, f, order_mode, order_value, first_trial, batch,
+                           _p(faulty), _p(order), threads)
+    if rc != 0:
+        raise RuntimeError(f"sliced gen rc={rc}")
+    return faulty, order

@@ -235,3 +235,38 @@ def test_om_recursion_at_m1_is_ba_py_rule(n):
     assert np.array_equal(dec_p, dec_t)
     assert np.array_equal(out_p, out_t)
     assert cnt_p == cnt_t
+
+
+# --- the word-sliced OpenMP port (oracle/ba_sliced.c) equals the recursion ----------
+SLICED_CASES = [(2, 1), (3, 1), (4, 1), (4, 2), (5, 3), (6, 6), (7, 2), (8, 5), (9, 4), (10, 0),
+                (10, 1), (10, 3), (11, 3), (12, 2), (13, 4), (16, 2), (20, 2), (32, 1)]
+
+
+@pytest.mark.parametrize("n,m", SLICED_CASES)
+def test_sliced_port_equals_recursion(n, m):
+    """bench.py's CPU baseline and the large-size checker (ba_sliced.c) against the
+    textbook recursion, on random, exact (beyond the bound) and dense faulty sets,
+    ragged batches, a non-zero first trial and 'other' orders."""
+    import oracle_c
+    B = 300 if n < 13 else 100
+    for fm, f, om in [(1, (n - 1) // 3, 1), (2, min(n, m + 1), 2), (1, n, 1)]:
+        kw = dict(seed=12345 + n, faulty_mode=fm, f=f, order_mode=om, order_value=2,
+                  first_trial=64 * 7)
+        d1, o1, c1 = oracle_c.run(n, m, B, **kw)
+        d2, o2, c2 = oracle_c.sliced_run(n, m, B, **kw)
+        assert np.array_equal(d1, d2) and np.array_equal(o1, o2) and c1 == c2, (n, m, fm, f, om)
+
+
+def test_sliced_port_given_inputs_and_n16_m5():
+    """Given inputs (sliced_gen staging) equal in-port draws; config 5's tree (n=16,
+    m=5) on three instances equals the recursion."""
+    import oracle_c
+    kw = dict(seed=0xBA5EED, faulty_mode=1, f=3, order_mode=1, first_trial=64 * 5)
+    fm, oc = oracle_c.sliced_gen(10, 1000, **kw)
+    a = oracle_c.sliced_run(10, 3, 1000, **kw)
+    b = oracle_c.sliced_run(10, 3, 1000, faulty=fm, order=oc, first_trial=64 * 5, seed=0xBA5EED)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]
+    kw = dict(seed=0xBA5EED, faulty_mode=1, f=5, order_mode=1, first_trial=64 * 3)
+    d1, o1, c1 = oracle_c.run(16, 5, 3, **kw)
+    d2, o2, c2 = oracle_c.sliced_run(16, 5, 3, **kw)
+    assert np.array_equal(d1, d2) and np.array_equal(o1, o2) and c1 == c2
