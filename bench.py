@@ -11,22 +11,29 @@ flip, ba.py:45, 269) is drawn from Philox in the kernel, every tree level and
 majority is resolved, every lieutenant's root decision is written to HBM
 (uint64/trial), plus the per-trial quorum/IC outcome byte and run counters.
 `value_with_input_generation` repeats the timing with the inputs drawn inside
-the kernel too.
+the kernel too.  Both passes follow a common warm-up of >= 1 s of back-to-back
+steps, so neither pays the clock ramp.
 
 N>1: launched one process per GPU by torch.distributed.run.  Trials shard by
 global index (weak scaling, no data-path collective); the run counters are
-all-reduced once over RCCL at the end of the timed region.
+all-reduced once over RCCL inside the C ABI (ba_comm_allreduce_device) at the
+end of the timed region.  torch.distributed (gloo) is the rendezvous only: the
+RCCL unique id, the barriers and the max-over-ranks of the wall time.
 
-Prints ONE JSON line (rank 0).  See DESIGN.md §Measurement for the roofline and
-cpu_baseline accounting.
+Prints ONE JSON line (rank 0).  DESIGN.md §5 gives the roofline accounting:
+`roofline` is the dominant kernel's HBM roofline on the bytes it must move
+(its per-trial inputs and outputs), `valu_roofline` its vector-issue roofline
+from the committed rocprofv3 counters of the same build, `compute_roofline`
+its Philox floor; the level-synchronous byte count of SURVEY.md §8d is kept as
+the labelled side figure `level_synchronous_equivalent`.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import platform
-import subprocess
 import sys
 import time
 
@@ -35,9 +42,30 @@ sys.path.insert(0, os.path.join(ROOT, "byzantine-agreement_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-# Philox4x32-10 issue ceiling of one MI355X (tools/philox_bench.hip, best code
-# shape: v_mad_u64_u32 + v_bitop3 xor3, 8 waves/SIMD; profiles/r01_philox_bench.jsonl)
-PHILOX_PEAK_CALLS = 9.69e11
+CLOCK_GHZ = 2.4        # MI355X_MICROARCH.md: max engine clock
+SIMDS = 1024           # 256 CUs x 4 SIMDs
+VALU_ISSUE_CYCLES = 2  # one wave64 VALU instruction per 2 cycles on a SIMD-32 (MI355X_MICROARCH.md)
+# Philox4x32-10 issue ceilings of one MI355X (tools/philox_bench.hip, the kernels'
+# code shape: v_mad_u64_u32 pairs + v_bitop3 xor3) by resident waves per SIMD
+PHILOX_PEAK_SRC = "profiles/r02_philox_bench.jsonl"
+PHILOX_PEAK_FALLBACK = {8: 9.69e11}
+# bytes one trial's own inputs and outputs occupy: faulty mask (u32) + order (u8)
+# read, decision word (u64) + outcome byte written (include/ba.h)
+IO_BYTES_IN, IO_BYTES_OUT = 5, 9
+
+
+def philox_peaks():
+    """{waves per SIMD: calls/s} from the committed philox_bench run."""
+    out = {}
+    try:
+        for line in open(os.path.join(ROOT, PHILOX_PEAK_SRC)):
+            d = json.loads(line)
+            if d.get("variant") == "xor3" and "waves_per_simd" in d:
+                w = int(d["waves_per_simd"])
+                out[w] = max(out.get(w, 0.0), float(d["philox_calls_per_s"]))
+    except (OSError, ValueError):
+        pass
+    return out or dict(PHILOX_PEAK_FALLBACK)
 
 
 def philox_calls_per_trial_word(n: int, m: int) -> int:
@@ -59,38 +87,44 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def algorithmic_bytes_per_trial(n: int, m: int) -> int:
-    """8 B per-trial I/O + 2 x ceil(bit-packed OM tree / 8)."""
+def level_synchronous_bytes_per_trial(n: int, m: int) -> int:
+    """8 B per-trial I/O + 2 x ceil(bit-packed OM tree / 8) -- what a
+    level-synchronous design (the LEVELS engine) writes and reads per trial."""
     from ba_amd import lib as L
     slots = L.load().ba_tree_slots(n, m)
     return 8 + 2 * ((slots + 7) // 8)
 
 
-def kernel_bytes(name: str, n: int, m: int, batch: int) -> int:
-    """Algorithmic HBM bytes of one launch of `name` over `batch` trials."""
+def kernel_io_bytes(name: str, n: int, m: int, batch: int, staged: bool) -> int:
+    """Algorithmic HBM bytes of one launch of `name` over `batch` trials: the bytes
+    the kernel cannot avoid moving."""
     from ba_amd import lib as L
     lib = L.load()
     me = L.effective_depth(n, m)
     S = [lib.ba_level_slots(n, m, k) for k in range(me + 1)]
     words = (batch + 63) // 64
-    if name == "k_relay_leaf":  # write L_me once, read L_{me-1} once
-        return 8 * words * (S[me] + S[me - 1])
-    if name == "k_majority_leaf":  # read L_me + L_{me-1}, write R_{me-1}
-        return 8 * words * (S[me] + 2 * S[me - 1])
+    if name.startswith("k_om") or name.startswith("k_fused"):  # tree on chip: per-trial I/O only
+        return (IO_BYTES_IN if staged else 0) * batch + IO_BYTES_OUT * batch
     if name == "k_leaf":  # levels me-1, me never materialised: read L_{me-2}, write R_{me-1}
         return 8 * words * (S[me - 2] + S[me - 1])
     if name == "k_relay_top":  # write levels 0..me-2 once
         return 8 * words * sum(S[: me - 1])
-    if name.startswith("k_fused") or name.startswith("k_om3w"):  # whole tree per launch
-        return algorithmic_bytes_per_trial(n, m) * batch
     return 0
 
 
-def pmc_traffic(n: int, m: int, batch: int, engine: str, kernel: str):
-    """HBM traffic per launch of `kernel` from the newest committed rocprofv3 PMC
-    summary of this exact workload (profiles/*pmc*.json, tools/pmc_summary.py;
-    FETCH_SIZE doubled per MI355X_MICROARCH.md), or (None, None, None)."""
+def so_digest() -> str:
+    """sha256 (16 hex) of the library this process runs: ties committed PMC counters
+    to the exact build (tools/pmc_summary.py records the same digest)."""
+    from ba_amd import lib as L
+    h = hashlib.sha256(open(L.LIB_PATH, "rb").read()).hexdigest()
+    return h[:16]
+
+
+def pmc_for(n, m, batch, engine, kernel, digest):
+    """Per-launch counters of `kernel` from the newest committed rocprofv3 PMC summary
+    of this workload (profiles/*pmc*.json).  Returns (entry, path, same_build)."""
     import glob
+    best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
         try:
             d = json.load(open(path))
@@ -101,29 +135,59 @@ def pmc_traffic(n: int, m: int, batch: int, engine: str, kernel: str):
             continue
         for name, e in d.get("kernels", {}).items():
             if kernel in name and "traffic_bytes" in e:
-                return e["traffic_bytes"], e.get("valu_util"), os.path.relpath(path, ROOT)
-    return None, None, None
+                same = d.get("lib_sha16") == digest
+                if same:
+                    return e, os.path.relpath(path, ROOT), True
+                if best is None:
+                    best = (e, os.path.relpath(path, ROOT), False)
+    return best if best else (None, None, False)
+
+
+def cpu_threads() -> int:
+    """The host threads this job may use: OMP_NUM_THREADS if the launcher set it (the
+    GPU pool sets it to the job's CPU share), else the process's CPU affinity."""
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
 
 
 def run_cpu_baseline(n, m, seed, fmax, budget_s):
-    """Time the C oracle (oracle/ba_oracle.c, OpenMP) on a bounded sample of the
-    same synthetic workload (same seed, first trials of the stream)."""
+    """Time the word-sliced OpenMP C port (oracle/ba_sliced.c: 64 trials per word,
+    one Philox call per two slot-words, the GPU engines' minimum draw count) on a
+    bounded sample of the same workload, inputs staged first as on the GPU."""
     import oracle_c
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     kw = dict(seed=seed, faulty_mode=1, f=fmax, order_mode=1)
-    probe = 64 * threads
+    probe = 64 * 64 * threads
+    fm, oc = oracle_c.sliced_gen(n, probe, threads=threads, **kw)
     t0 = time.perf_counter()
-    oracle_c.run(n, m, probe, threads=threads, **kw)
-    dt = time.perf_counter() - t0
-    rate = probe / max(dt, 1e-9)
-    sample = int(min(max(rate * budget_s, probe), 1 << 22)) // 64 * 64
+    oracle_c.sliced_run(n, m, probe, seed=seed, faulty=fm, order=oc, threads=threads)
+    rate = probe / max(time.perf_counter() - t0, 1e-9)
+    sample = int(min(max(rate * budget_s, probe), 1 << 27)) // 64 * 64
+    fm, oc = oracle_c.sliced_gen(n, sample, threads=threads, **kw)
     t0 = time.perf_counter()
-    oracle_c.run(n, m, sample, threads=threads, **kw)
+    _, _, c = oracle_c.sliced_run(n, m, sample, seed=seed, faulty=fm, order=oc, threads=threads)
     dt = time.perf_counter() - t0
-    return {"value": sample / dt, "unit": "trial-decisions/s", "cores": threads, "kind": "port",
-            "sample": f"C oracle (oracle/ba_oracle.c, OpenMP x{threads}) on the first {sample} "
-                      f"trials of the same n={n}, m={m} synthetic stream, {dt:.1f} s; "
-                      f"host CPU: {cpu_model()}, nproc={os.cpu_count()}"}
+    value = sample / dt
+    nproc = os.cpu_count() or 1
+    return {"value": round(value, 1), "unit": "trial-decisions/s", "cores": threads, "kind": "port",
+            "sample": f"word-sliced OpenMP C port (oracle/ba_sliced.c, x{threads} threads) on the "
+                      f"first {sample} trials of the same n={n}, m={m} synthetic stream (inputs "
+                      f"staged first, as on the GPU), {dt:.1f} s; host CPU: {cpu_model()}, "
+                      f"nproc={nproc}; {threads} threads = this job's CPU share "
+                      f"(OMP_NUM_THREADS / affinity)",
+            "per_thread_value": round(value / threads, 1),
+            "all_cores_projection": {"value": round(value / threads * nproc, 1), "cores": nproc,
+                                     "note": "per-thread rate x nproc, not measured (the pool "
+                                             "grants this job its CPU share only)"},
+            "counters_trials": c["trials"],
+            "reference_ba_py": {"value_us_per_trial": 574.0, "config": "OM(1) n=10, one core",
+                                "where": "dev container (Intel Xeon), BASELINE.md; ba.py cannot "
+                                         "run on the GPU box (rpyc and the reference are absent)"}}
 
 
 def main():
@@ -137,7 +201,9 @@ def main():
     ap.add_argument("--fmax", type=int, default=-1)
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0xBA5EED)
     ap.add_argument("--engine", default="auto", choices=["auto", "fused", "levels"])
-    ap.add_argument("--cpu-budget-s", type=float, default=16.0)
+    ap.add_argument("--warm-s", type=float, default=1.0,
+                    help="common warm-up: back-to-back steps before any timed pass")
+    ap.add_argument("--cpu-budget-s", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--inputs-in-kernel", action="store_true",
@@ -150,26 +216,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    # rehearsal knobs for a one-GPU box (never set by the driver): every rank on
-    # cuda:0 and gloo in place of RCCL, which refuses two ranks on one device
-    backend = os.environ.get("BA_BENCH_BACKEND", "nccl")
-    if os.environ.get("BA_BENCH_SHARE_GPU") == "1":
-        local = 0
+    dist = comm = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+        dist.init_process_group("gloo")  # rendezvous, barriers, wall-time max; RCCL is in the C ABI
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     n, m, B = args.n, args.m, args.batch
     fmax = L.default_fmax(n) if args.fmax < 0 else args.fmax
     engine_id = {"auto": L.ENGINE_AUTO, "fused": L.ENGINE_FUSED, "levels": L.ENGINE_LEVELS}[args.engine]
     eng = L.Engine(dev.index)
+    if world > 1:
+        from ba_amd import dist as D
+        comm = D.init_comm(eng)
     dec = torch.empty(B, dtype=torch.int64, device=dev)
     out = torch.empty(B, dtype=torch.uint8, device=dev)
     cnt = torch.zeros(16, dtype=torch.int64, device=dev)
@@ -177,112 +236,150 @@ def main():
     # the HIP events below bracket exactly the hot-path kernels
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
+    sp = stream.cuda_stream
 
     def first_of(i):
         return (i * world + rank) * B  # global trial index: weak scaling, disjoint shards
 
-    def rand_params(i):
-        return L.make_params(n, m, args.seed, L.LIE_PHILOX, L.FAULTY_RANDOM, fmax, L.ORDER_RANDOM,
-                             L.ATTACK, engine_id, first_of(i))
-
-    # stage every step's inputs in HBM before any timing (ba_gen_inputs_device)
-    n_steps_total = args.warmup + 2 * args.steps
-    staged = {}
+    # every step's inputs staged in HBM and every step's params built before timing
+    n_warm_slots = args.warmup + 2
+    n_total = n_warm_slots + 3 * args.steps
+    staged_params, gen_params, staged = [], [], []
     if not args.inputs_in_kernel:
-        fbuf = torch.empty((n_steps_total, B), dtype=torch.int32, device=dev)
-        obuf = torch.empty((n_steps_total, B), dtype=torch.uint8, device=dev)
-        for i in range(n_steps_total):
-            eng.gen_inputs_device(rand_params(i), B, d_faulty=fbuf[i].data_ptr(),
-                                  d_order=obuf[i].data_ptr(), stream=stream.cuda_stream)
-            staged[i] = (fbuf[i].data_ptr(), obuf[i].data_ptr())
-        torch.cuda.synchronize(dev)
+        fbuf = torch.empty((n_total, B), dtype=torch.int32, device=dev)
+        obuf = torch.empty((n_total, B), dtype=torch.uint8, device=dev)
+    for i in range(n_total):
+        gp = L.make_params(n, m, args.seed, L.LIE_PHILOX, L.FAULTY_RANDOM, fmax, L.ORDER_RANDOM,
+                           L.ATTACK, engine_id, first_of(i))
+        gen_params.append(gp)
+        if not args.inputs_in_kernel:
+            eng.gen_inputs_device(gp, B, d_faulty=fbuf[i].data_ptr(), d_order=obuf[i].data_ptr(),
+                                  stream=sp)
+            staged.append((fbuf[i].data_ptr(), obuf[i].data_ptr()))
+            staged_params.append(L.make_params(n, m, args.seed, L.LIE_PHILOX, L.FAULTY_GIVEN, fmax,
+                                               L.ORDER_GIVEN, L.ATTACK, engine_id, first_of(i)))
+    torch.cuda.synchronize(dev)
+    dptr, optr, cptr = dec.data_ptr(), out.data_ptr(), cnt.data_ptr()
 
-    def step(i, in_kernel=args.inputs_in_kernel):
+    def step(i, in_kernel):
         if in_kernel:
-            p = rand_params(i)
-            eng.run_device(p, B, d_decisions=dec.data_ptr(), d_outcome=out.data_ptr(),
-                           d_counters=cnt.data_ptr(), stream=stream.cuda_stream)
+            eng.run_device(gen_params[i], B, d_decisions=dptr, d_outcome=optr, d_counters=cptr,
+                           stream=sp)
         else:
-            p = L.make_params(n, m, args.seed, L.LIE_PHILOX, L.FAULTY_GIVEN, fmax, L.ORDER_GIVEN,
-                              L.ATTACK, engine_id, first_of(i))
             fp, op = staged[i]
-            eng.run_device(p, B, d_faulty=fp, d_order=op, d_decisions=dec.data_ptr(),
-                           d_outcome=out.data_ptr(), d_counters=cnt.data_ptr(),
-                           stream=stream.cuda_stream)
+            eng.run_device(staged_params[i], B, d_faulty=fp, d_order=op, d_decisions=dptr,
+                           d_outcome=optr, d_counters=cptr, stream=sp)
 
-    def timed(in_kernel):
+    # common warm-up: >= warm_s of back-to-back steps (both modes) before any timing,
+    # so the first timed pass does not pay the clock / power ramp
+    t_w = time.perf_counter()
+    k = 0
+    while True:
         for i in range(args.warmup):
-            step(i, in_kernel)
+            step(i, args.inputs_in_kernel)
+            if not args.inputs_in_kernel:
+                step(args.warmup + 1, True)
+        torch.cuda.synchronize(dev)
+        k += 1
+        if time.perf_counter() - t_w >= args.warm_s and k >= 1:
+            break
+    warm_s = time.perf_counter() - t_w
+
+    def timed(base, in_kernel):
         cnt.zero_()
         torch.cuda.synchronize(dev)
         if dist:
             dist.barrier()
         torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
         ev0.record(stream)
         for i in range(args.steps):
-            step(args.warmup + i, in_kernel)
-        if dist:
-            dist.all_reduce(cnt)  # the only collective: run counters (RCCL)
+            step(base + i, in_kernel)
         ev1.record(stream)
+        if comm is not None:
+            comm.allreduce_device(cptr, stream=sp)  # the only collective: run counters (RCCL)
         torch.cuda.synchronize(dev)
         if dist:
             dist.barrier()
-        torch.cuda.synchronize(dev)
         wall = time.perf_counter() - t0
-        elapsed = torch.tensor([wall], dtype=torch.float64, device=dev)
+        elapsed = torch.tensor([wall], dtype=torch.float64)
         if dist:
             dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
         return float(elapsed.item()), ev0.elapsed_time(ev1)
 
     total_trials = B * args.steps * world
-    T, gpu_ms = timed(args.inputs_in_kernel)
+    base = n_warm_slots
+    T, gpu_ms = timed(base, args.inputs_in_kernel)
     counters = dict(zip(L.COUNTER_NAMES, [int(x) for x in cnt.cpu().tolist()]))
     value = total_trials / T
-    value_gen = None
+    value_gen = gen_ms = None
     if not args.inputs_in_kernel:
-        T2, _ = timed(True)
+        T2, gen_ms = timed(base, True)  # same trials, inputs drawn in the kernel
         counters2 = dict(zip(L.COUNTER_NAMES, [int(x) for x in cnt.cpu().tolist()]))
         if counters2 != counters:
             raise SystemExit(f"staged-input and in-kernel-input runs disagree: {counters} vs {counters2}")
         value_gen = total_trials / T2
 
-    # per-kernel HIP-event timing on the launch stream (a second pass of the same steps)
-    kernels, roof, compute_roof = {}, None, None
+    # per-kernel HIP-event timing on the launch stream (a further pass of new steps)
+    kernels, roof, valu_roof, compute_roof, side = {}, None, None, None, None
+    staged_mode = not args.inputs_in_kernel
     if not args.no_profile:
         eng.profile(True)
         for i in range(args.steps):
-            step(args.warmup + args.steps + i)
+            step(base + args.steps + i, args.inputs_in_kernel)
         torch.cuda.synchronize(dev)
         kernels = eng.profile_read()
         eng.profile(False)
-        if kernels:
-            name, (nl, ms) = max(kernels.items(), key=lambda kv: kv[1][1])
-            avg_ms = ms / nl
-            alg = kernel_bytes(name, n, m, B)
-            achieved = alg / (avg_ms * 1e-3) / 1e9 if alg else None
-            traffic, valu, src = pmc_traffic(n, m, B, args.engine, name)
-            roof = {"bound": "hbm", "kernel": name, "avg_ms": round(avg_ms, 4),
-                    "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                    "traffic": round(traffic) if traffic else None,
-                    "algorithmic_bytes_per_launch": alg,
-                    "traffic_source": src,
-                    "valu_util": round(valu, 4) if valu else None,
-                    "note": "algorithmic bytes = SURVEY.md 8d's level-synchronous figure; the "
-                            "fused kernel keeps the tree in LDS/registers, so frac > 1 means it "
-                            "beats that design, and compute_roofline is its real bound"}
-            words = (B + 63) // 64
-            calls = philox_calls_per_trial_word(n, m) * words
-            rate = calls / (avg_ms * 1e-3)
-            compute_roof = {"bound": "valu (Philox4x32-10 lie draws)", "kernel": name,
-                            "achieved": round(rate / 1e9, 2), "peak": round(PHILOX_PEAK_CALLS / 1e9, 2),
-                            "unit": "G Philox calls/s", "frac": round(rate / PHILOX_PEAK_CALLS, 4),
-                            "calls_per_launch": calls,
-                            "floor_ms": round(calls / PHILOX_PEAK_CALLS * 1e3, 4),
-                            "peak_source": "profiles/r01_philox_bench.jsonl"}
+    if kernels:
+        name, (nl, ms) = max(kernels.items(), key=lambda kv: kv[1][1])
+        avg_ms = ms / nl
+        digest = so_digest()
+        pmc, pmc_src, same_build = pmc_for(n, m, B, args.engine, name, digest)
+        io = kernel_io_bytes(name, n, m, B, staged_mode)
+        achieved = io / (avg_ms * 1e-3) / 1e9
+        traffic = pmc["traffic_bytes"] if pmc else None
+        roof = {"bound": "hbm", "kernel": name, "avg_ms": round(avg_ms, 4),
+                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": round(traffic) if traffic else None,
+                "traffic_frac": round(traffic / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+                "algorithmic_bytes_per_launch": io,
+                "algorithmic_bytes_per_trial": io / B,
+                "traffic_source": pmc_src, "traffic_same_build": same_build,
+                "note": "bytes the kernel must move: per-trial inputs (5 B, staged) and outputs "
+                        "(9 B); the OM tree lives in LDS/registers, so HBM is not this kernel's "
+                        "bound -- valu_roofline is"}
+        if pmc and pmc.get("counters", {}).get("SQ_INSTS_VALU"):
+            insts = pmc["counters"]["SQ_INSTS_VALU"]
+            cycles = avg_ms * 1e-3 * CLOCK_GHZ * 1e9
+            valu_roof = {"bound": "valu", "kernel": name,
+                         "achieved": round(insts * VALU_ISSUE_CYCLES / (avg_ms * 1e-3) / 1e9, 1),
+                         "peak": round(SIMDS * CLOCK_GHZ, 1), "unit": "G SIMD-cycles/s",
+                         "frac": round(insts * VALU_ISSUE_CYCLES / (SIMDS * cycles), 4),
+                         "valu_insts_per_launch": insts,
+                         "formula": "SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x 2.4 GHz x avg launch)",
+                         "source": pmc_src, "same_build": same_build}
+        words = (B + 63) // 64
+        calls = philox_calls_per_trial_word(n, m) * words
+        rate = calls / (avg_ms * 1e-3)
+        peaks = philox_peaks()
+        wps = 2 if name.startswith("k_om") else max(peaks)
+        peak = peaks.get(wps, max(peaks.values()))
+        compute_roof = {"bound": "valu (Philox4x32-10 lie draws)", "kernel": name,
+                        "achieved": round(rate / 1e9, 2), "peak": round(peak / 1e9, 2),
+                        "unit": "G Philox calls/s", "frac": round(rate / peak, 4),
+                        "peak_waves_per_simd": wps,
+                        "peaks_by_waves_per_simd": {str(k): round(v / 1e9, 2) for k, v in sorted(peaks.items())},
+                        "calls_per_launch": calls, "floor_ms": round(calls / peak * 1e3, 4),
+                        "peak_source": PHILOX_PEAK_SRC}
+        lsb = level_synchronous_bytes_per_trial(n, m) * B
+        side = {"bytes_per_launch": lsb, "bytes_per_trial": lsb / B,
+                "equivalent_gbs": round(lsb / (avg_ms * 1e-3) / 1e9, 1),
+                "note": "SURVEY.md 8d's level-synchronous bytes (each bit-packed tree level written "
+                        "once and read once): moved by the LEVELS engine, NOT by this kernel; a "
+                        "comparison figure only"}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = run_cpu_baseline(n, m, args.seed, fmax, args.cpu_budget_s)
@@ -300,15 +397,22 @@ def main():
                        "parallelism": f"trial-dp{world}"},
             "inputs": "in-kernel Philox draws" if args.inputs_in_kernel else
                       "staged in HBM before the timed region (ba_gen_inputs_device); lies drawn in-kernel",
+            "ms_per_step_gpu_events": round(gpu_ms / args.steps, 4),
+            "value_gpu_events": round(B * args.steps / (gpu_ms * 1e-3), 1),
             "value_with_input_generation": round(value_gen, 1) if value_gen else None,
-            "gpu_event_ms": round(gpu_ms, 3),
+            "ms_per_step_with_input_generation_gpu_events": round(gen_ms / args.steps, 4) if gen_ms else None,
+            "warm_up_s": round(warm_s, 2),
             "kernels_ms": {k: round(v[1] / v[0], 4) for k, v in kernels.items()},
             "roofline": roof,
+            "valu_roofline": valu_roof,
             "compute_roofline": compute_roof,
+            "level_synchronous_equivalent": side,
             "cpu_baseline": cpu,
             "counters": counters,
         }
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
     if dist:
         dist.destroy_process_group()
     eng.close()

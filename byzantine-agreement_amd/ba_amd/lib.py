@@ -37,7 +37,9 @@ EXPORTS = ["ba_version", "ba_device_count", "ba_ctx_create", "ba_ctx_destroy", "
            "ba_om1_coin_count", "ba_mt_draw_coins", "ba_mt_table", "ba_vote_slots",
            "ba_subtree_votes_device", "ba_root_from_votes_device", "ba_gen_inputs_device",
            "ba_ctx_device", "ba_comm_unique_id", "ba_comm_create", "ba_comm_destroy",
-           "ba_trial_share", "ba_run_trials_multi"]
+           "ba_trial_share", "ba_run_trials_multi", "ba_comm_rank", "ba_subtree_share",
+           "ba_comm_allreduce_device", "ba_comm_allgather_votes_device",
+           "ba_run_instance_split_multi"]
 
 
 class BAError(RuntimeError):
@@ -129,6 +131,12 @@ def load(path: str | None = None):
     lib.ba_run_trials_multi.argtypes = [vp, vp, ctypes.POINTER(Params), u64, vp, vp,
                                         ctypes.POINTER(Counters), ctypes.POINTER(u64),
                                         ctypes.POINTER(u64)]
+    lib.ba_comm_rank.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
+    lib.ba_subtree_share.argtypes = [u32, i32, i32, ctypes.POINTER(u32), ctypes.POINTER(u32)]
+    lib.ba_comm_allreduce_device.argtypes = [vp, vp, vp]
+    lib.ba_comm_allgather_votes_device.argtypes = [vp, u32, u32, u64, vp, vp]
+    lib.ba_run_instance_split_multi.argtypes = [vp, vp, ctypes.POINTER(Params), u64, vp, vp, vp,
+                                                vp, ctypes.POINTER(Counters)]
     if lib.ba_version() != ABI_VERSION:
         raise RuntimeError(f"libba_hip ABI {lib.ba_version()} != {ABI_VERSION}")
     if path is None:
@@ -285,6 +293,14 @@ def trial_share(total_trials: int, nranks: int, rank: int):
     return f.value, c.value
 
 
+def subtree_share(n: int, nranks: int, rank: int):
+    """[j_begin, j_end) first-hop subtrees of rank (ba_subtree_share)."""
+    lib = load()
+    b, e = ctypes.c_uint32(), ctypes.c_uint32()
+    _check(lib, lib.ba_subtree_share(n, nranks, rank, ctypes.byref(b), ctypes.byref(e)))
+    return b.value, e.value
+
+
 class Comm:
     """An RCCL communicator owned by the C ABI (ba_comm_create) on an Engine's
     device: ba_run_trials_multi shards trials over the ranks and all-reduces
@@ -296,8 +312,21 @@ class Comm:
         _check(self.lib, self.lib.ba_comm_create(engine.handle, nranks, rank, uid, ctypes.byref(h)))
         self.handle = h
 
+    @property
+    def rank(self):
+        nr, r = ctypes.c_int(), ctypes.c_int()
+        _check(self.lib, self.lib.ba_comm_rank(self.handle, ctypes.byref(nr), ctypes.byref(r)))
+        return r.value
+
+    @property
+    def nranks(self):
+        nr, r = ctypes.c_int(), ctypes.c_int()
+        _check(self.lib, self.lib.ba_comm_rank(self.handle, ctypes.byref(nr), ctypes.byref(r)))
+        return nr.value
+
     def run_trials(self, params: Params, total_trials: int, d_decisions=0, d_outcome=0):
-        """-> (whole-job counters dict, share first, share count)."""
+        """Trial-DP job (ba_run_trials_multi) -> (whole-job counters dict, share first,
+        share count)."""
         cnt = Counters()
         f, c = ctypes.c_uint64(), ctypes.c_uint64()
         _check(self.lib, self.lib.ba_run_trials_multi(
@@ -305,6 +334,25 @@ class Comm:
             d_decisions or None, d_outcome or None, ctypes.byref(cnt), ctypes.byref(f),
             ctypes.byref(c)))
         return dict(zip(COUNTER_NAMES, [int(x) for x in cnt.v])), f.value, c.value
+
+    def run_instance_split(self, params: Params, batch: int, d_decisions=0, d_outcome=0,
+                           d_faulty=0, d_order=0):
+        """First-hop split job (ba_run_instance_split_multi) -> counters dict (same on
+        every rank); decisions / outcome (batch entries) to the device buffers."""
+        cnt = Counters()
+        _check(self.lib, self.lib.ba_run_instance_split_multi(
+            self.engine.handle, self.handle, ctypes.byref(params), batch, d_faulty or None,
+            d_order or None, d_decisions or None, d_outcome or None, ctypes.byref(cnt)))
+        return dict(zip(COUNTER_NAMES, [int(x) for x in cnt.v]))
+
+    def allreduce_device(self, d_counters: int, stream=0):
+        """Sum the 16 device counters over the ranks in place (async on stream)."""
+        _check(self.lib, self.lib.ba_comm_allreduce_device(self.handle, d_counters, stream or None))
+
+    def allgather_votes_device(self, n: int, m: int, batch: int, d_votes: int, stream=0):
+        """Every rank's subtree-vote rows to every rank, in place (async on stream)."""
+        _check(self.lib, self.lib.ba_comm_allgather_votes_device(self.handle, n, m, batch,
+                                                                 d_votes, stream or None))
 
     def close(self):
         if self.handle:

@@ -211,11 +211,40 @@ struct ba_ctx {
     size_t scratch_budget = 8ull << 30;
     bool leaf_fusion = true;  // LEVELS uses k_leaf when available (BA_NO_LEAF_FUSION=1: off)
     DevBuf scratch, partials, io_faulty, io_order, io_table, io_poll, io_dec, io_out, io_cnt;
-    DevBuf sink;  // counter sink replicas + tickets (zeroed once; kernels leave them zero)
+    DevBuf sink;  // counter sink replicas (zeroed once; kernels leave them zero)
     std::map<uint64_t, std::unique_ptr<GeoEntry>> geos;
     Prof prof;
     std::map<std::string, ProfTotal> prof_totals;
+    // Stream ordering of the calls that share the ctx's scratch and counter sink:
+    // the event marks the end of the last such call, on last_stream.
+    hipEvent_t last_ev = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool have_last = false;
 };
+
+// A call about to use the ctx's scratch / sink on stream `s` first waits for
+// the ctx's previous call if that ran on another stream (include/ba.h: calls of
+// one ctx may come from any streams; the library orders them itself).  Skipped
+// while `s` is capturing a graph: the replay's ordering is the caller's.
+static bool stream_capturing(hipStream_t s) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+
+static hipError_t ctx_order(ba_ctx* ctx, hipStream_t s) {
+    if (!ctx->have_last || ctx->last_stream == s || stream_capturing(s)) return hipSuccess;
+    return hipStreamWaitEvent(s, ctx->last_ev, 0);
+}
+
+static hipError_t ctx_mark(ba_ctx* ctx, hipStream_t s) {
+    if (stream_capturing(s)) return hipSuccess;
+    hipError_t e = hipEventRecord(ctx->last_ev, s);
+    if (e == hipSuccess) {
+        ctx->last_stream = s;
+        ctx->have_last = true;
+    }
+    return e;
+}
 
 namespace ba {
 hipEvent_t Prof::take() {
@@ -308,13 +337,16 @@ extern "C" int ba_ctx_create(int device, ba_ctx** out) {
     if (const char* s = getenv("BA_SCRATCH_BYTES")) ctx->scratch_budget = strtoull(s, nullptr, 0);
     if (const char* s = getenv("BA_NO_LEAF_FUSION")) ctx->leaf_fusion = strcmp(s, "1") != 0;
     hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->last_ev, hipEventDisableTiming);
     if (e != hipSuccess) {
+        if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
         delete ctx;
-        return fail(BA_EDEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
+        return fail(BA_EDEVICE, "hipStreamCreate/hipEventCreate: %s", hipGetErrorString(e));
     }
     if (ctx->sink.grow(kSinkBytes) != BA_OK || hipMemset(ctx->sink.p, 0, kSinkBytes) != hipSuccess ||
         hipDeviceSynchronize() != hipSuccess) {
         (void)hipStreamDestroy(ctx->stream);
+        (void)hipEventDestroy(ctx->last_ev);
         ctx->sink.release();
         delete ctx;
         return fail(BA_ENOMEM, "counter sink allocation failed");
@@ -344,6 +376,7 @@ extern "C" void ba_ctx_destroy(ba_ctx* ctx) {
         kv.second->members.release();
     }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->last_ev) (void)hipEventDestroy(ctx->last_ev);
     delete ctx;
 }
 
@@ -400,6 +433,11 @@ static int validate(const ba_params* p, uint64_t batch, bool has_faulty, bool ha
         if (batch && !has_table) return fail(BA_EINVAL, "BA_LIE_TABLE needs lie_table");
     }
     return BA_OK;
+}
+
+// ba_multi.cpp validates a whole job on every rank before its collectives
+extern "C" int ba_validate_internal(const ba_params* p, uint64_t batch) {
+    return validate(p, batch, true, true, true);
 }
 
 static GeoEntry* geometry(ba_ctx* ctx, uint32_t n, uint32_t me, int* rc) {
@@ -472,7 +510,6 @@ static RunArgs make_args(ba_ctx* ctx, const ba_params* p, uint64_t batch, const 
     a.prof = &ctx->prof;
     a.cu_count = ctx->cu_count;
     a.sink.rep = (unsigned long long*)ctx->sink.p;
-    a.sink.ticket = (unsigned int*)((char*)ctx->sink.p + kSinkReplicas * kSinkRepStride * 8);
     return a;
 }
 
@@ -511,12 +548,11 @@ static int run_levels(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge, const LevelsJ
     return BA_OK;
 }
 
-extern "C" int ba_run_trials_device(ba_ctx* ctx, const ba_params* p, uint64_t batch,
-                                    const uint32_t* d_faulty, const uint8_t* d_order,
-                                    const uint32_t* d_table, const uint32_t* d_poll,
-                                    uint64_t* d_decisions, uint8_t* d_outcome,
-                                    uint64_t* d_counters, void* stream) {
-    if (!ctx) return fail(BA_EINVAL, "ctx is NULL");
+static int run_trials_device_impl(ba_ctx* ctx, const ba_params* p, uint64_t batch,
+                                  const uint32_t* d_faulty, const uint8_t* d_order,
+                                  const uint32_t* d_table, const uint32_t* d_poll,
+                                  uint64_t* d_decisions, uint8_t* d_outcome, uint64_t* d_counters,
+                                  void* stream) {
     int rc = validate(p, batch, d_faulty != nullptr, d_order != nullptr, d_table != nullptr);
     if (rc != BA_OK) return rc;
     if (!d_counters) return fail(BA_EINVAL, "d_counters is required on the device path");
@@ -587,9 +623,9 @@ static int validate_split(ba_ctx* ctx, const ba_params* p, uint64_t batch, const
     return BA_OK;
 }
 
-extern "C" int ba_subtree_votes_device(ba_ctx* ctx, const ba_params* p, uint64_t batch,
-                                       uint32_t j_begin, uint32_t j_end, const uint32_t* d_faulty,
-                                       const uint8_t* d_order, uint64_t* d_votes, void* stream) {
+static int subtree_votes_impl(ba_ctx* ctx, const ba_params* p, uint64_t batch, uint32_t j_begin,
+                              uint32_t j_end, const uint32_t* d_faulty, const uint8_t* d_order,
+                              uint64_t* d_votes, void* stream) {
     int rc = validate_split(ctx, p, batch, d_faulty, d_order);
     if (rc != BA_OK) return rc;
     if (j_begin >= j_end || j_end > p->n - 1)
@@ -608,10 +644,10 @@ extern "C" int ba_subtree_votes_device(ba_ctx* ctx, const ba_params* p, uint64_t
     return run_levels(ctx, a, ge, job, j_begin, j_end, true, nullptr);
 }
 
-extern "C" int ba_root_from_votes_device(ba_ctx* ctx, const ba_params* p, uint64_t batch,
-                                         const uint32_t* d_faulty, const uint8_t* d_order,
-                                         const uint64_t* d_votes, uint64_t* d_decisions,
-                                         uint8_t* d_outcome, uint64_t* d_counters, void* stream) {
+static int root_from_votes_impl(ba_ctx* ctx, const ba_params* p, uint64_t batch,
+                                const uint32_t* d_faulty, const uint8_t* d_order,
+                                const uint64_t* d_votes, uint64_t* d_decisions, uint8_t* d_outcome,
+                                uint64_t* d_counters, void* stream) {
     int rc = validate_split(ctx, p, batch, d_faulty, d_order);
     if (rc != BA_OK) return rc;
     if (!d_votes || !d_counters) return fail(BA_EINVAL, "d_votes and d_counters are required");
@@ -630,6 +666,49 @@ extern "C" int ba_root_from_votes_device(ba_ctx* ctx, const ba_params* p, uint64
     return run_levels(ctx, a, ge, job, 0, 0, true, (uint64_t*)ctx->partials.p);
 }
 
+// The ordered entry points: wait for the ctx's previous call if it ran on
+// another stream, then mark this call's end (ctx_order / ctx_mark).
+template <typename F>
+static int ordered(ba_ctx* ctx, void* stream, F&& body) {
+    if (!ctx) return fail(BA_EINVAL, "ctx is NULL");
+    const hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(ctx_order(ctx, s));
+    const int rc = body();
+    if (rc == BA_OK) HIP_TRY(ctx_mark(ctx, s));
+    return rc;
+}
+
+extern "C" int ba_run_trials_device(ba_ctx* ctx, const ba_params* p, uint64_t batch,
+                                    const uint32_t* d_faulty, const uint8_t* d_order,
+                                    const uint32_t* d_table, const uint32_t* d_poll,
+                                    uint64_t* d_decisions, uint8_t* d_outcome,
+                                    uint64_t* d_counters, void* stream) {
+    return ordered(ctx, stream, [&] {
+        return run_trials_device_impl(ctx, p, batch, d_faulty, d_order, d_table, d_poll,
+                                      d_decisions, d_outcome, d_counters, stream);
+    });
+}
+
+extern "C" int ba_subtree_votes_device(ba_ctx* ctx, const ba_params* p, uint64_t batch,
+                                       uint32_t j_begin, uint32_t j_end, const uint32_t* d_faulty,
+                                       const uint8_t* d_order, uint64_t* d_votes, void* stream) {
+    return ordered(ctx, stream, [&] {
+        return subtree_votes_impl(ctx, p, batch, j_begin, j_end, d_faulty, d_order, d_votes,
+                                  stream);
+    });
+}
+
+extern "C" int ba_root_from_votes_device(ba_ctx* ctx, const ba_params* p, uint64_t batch,
+                                         const uint32_t* d_faulty, const uint8_t* d_order,
+                                         const uint64_t* d_votes, uint64_t* d_decisions,
+                                         uint8_t* d_outcome, uint64_t* d_counters, void* stream) {
+    return ordered(ctx, stream, [&] {
+        return root_from_votes_impl(ctx, p, batch, d_faulty, d_order, d_votes, d_decisions,
+                                    d_outcome, d_counters, stream);
+    });
+}
+
 // ---------------------------------------------------------------------------
 // host entry point: copy in, run, copy out (PCIe-inclusive)
 // ---------------------------------------------------------------------------
@@ -644,6 +723,7 @@ extern "C" int ba_run_trials(ba_ctx* ctx, const ba_params* p, uint64_t batch,
     if (batch == 0) return BA_OK;
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
+    HIP_TRY(ctx_order(ctx, st));  // the io buffers follow the ctx's last call
     const bool need_f = p->faulty_mode == BA_FAULTY_GIVEN, need_o = p->order_mode == BA_ORDER_GIVEN;
     const bool need_t = p->lie_mode == BA_LIE_TABLE, need_p = need_t && poll;
     if (need_f && (rc = ctx->io_faulty.grow(batch * 4)) != BA_OK) return rc;

@@ -417,20 +417,29 @@ __device__ __forceinline__ void wave_counts_add(bool live, const TrialResult& r,
 // caller's 12 counters (one line) at the end of a launch serialise: measured
 // ~130 us for 2048 waves x 12 single-lane adds.  Instead each reporting unit
 // (a wave or a block) adds its totals with ONE 12-lane instruction into
-// replica (unit % R), every replica on lines of its own, then takes a ticket
-// on that replica; the unit whose ticket completes the replica reads it back
-// with atomic exchanges (resetting it for the next launch) and adds it into
-// the caller's counters.  At most R units touch the caller's line.
+// replica (unit % R), every replica on a line of its own, and only the last
+// unit of a replica folds it into the caller's counters: at most R units
+// touch the caller's line.
+//
+// Memory ordering needs no fence: every replica word carries its own arrival
+// count in its top 16 bits (each unit adds v + 2^48), so the unit whose
+// returning add sees members-1 earlier arrivals on a word holds that word's
+// complete sum -- an ordering on ONE location, which relaxed device-scope
+// atomics guarantee (coherence order), unlike the ticket-on-another-word
+// scheme it replaces, which relied on s_waitcnt draining the adds before the
+// ticket.  That unit resets the word with an atomic exchange (no later
+// access to it in this launch) and adds the sum into `out`.  Sums per launch
+// and replica stay below 2^48; units per replica below 2^16.
 // Units of one launch must all call sink_counters exactly once.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSinkReplicas = 64;
-constexpr uint32_t kSinkRepStride = 16;     // uint64 per replica (128 B)
-constexpr uint32_t kSinkTicketStride = 32;  // uint32 per ticket (128 B)
-constexpr size_t kSinkBytes = kSinkReplicas * (kSinkRepStride * 8 + kSinkTicketStride * 4);
+constexpr uint32_t kSinkRepStride = 16;  // uint64 per replica (128 B)
+constexpr size_t kSinkBytes = kSinkReplicas * kSinkRepStride * 8;
+constexpr uint32_t kSinkArrivalShift = 48;
+constexpr unsigned long long kSinkValueMask = (1ull << kSinkArrivalShift) - 1;
 
 struct Sink {
     unsigned long long* rep;  // [kSinkReplicas][kSinkRepStride], zero between launches
-    unsigned int* ticket;     // [kSinkReplicas][kSinkTicketStride], zero between launches
 };
 
 // Called by every lane of one wave; lane c < C_NUM passes the unit's total of
@@ -440,18 +449,18 @@ __device__ __forceinline__ void sink_counters(uint32_t lane, uint64_t v, uint32_
                                               const Sink& sk) {
     const uint32_t r = unit % kSinkReplicas;
     const uint32_t members = (nunits - r + kSinkReplicas - 1) / kSinkReplicas;
-    unsigned long long* rep = sk.rep + r * kSinkRepStride;
-    if (lane < C_NUM && v) atomicAdd(rep + lane, (unsigned long long)v);
-    __builtin_amdgcn_s_waitcnt(0);  // the adds are performed before the ticket
-    uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(sk.ticket + r * kSinkTicketStride, 1u);
-    t = __shfl(t, 0, 64);
-    if (t + 1 == members) {  // last unit of this replica: fold it into `out`
-        if (lane < C_NUM) {
-            const unsigned long long tot = atomicExch(rep + lane, 0ull);
-            if (tot) atomicAdd((unsigned long long*)out + lane, tot);
+    if (lane < C_NUM) {
+        unsigned long long* w = sk.rep + r * kSinkRepStride + lane;
+        const unsigned long long old =
+            __hip_atomic_fetch_add(w, (unsigned long long)v + (1ull << kSinkArrivalShift),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(old >> kSinkArrivalShift) + 1u == members) {
+            const unsigned long long tot = (old + v) & kSinkValueMask;
+            (void)__hip_atomic_exchange(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tot)
+                (void)__hip_atomic_fetch_add((unsigned long long*)out + lane, tot, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (lane == 0) atomicExch(sk.ticket + r * kSinkTicketStride, 0u);
     }
 }
 

@@ -1,13 +1,27 @@
-// ba_multi.cpp -- trial data-parallel runs across GPUs inside the C ABI
-// (ba_run_trials_multi owns the RCCL communicators), for a
-// host binding that does not bring torch.distributed.  One process per GPU:
-// rank 0 makes a unique id (ba_comm_unique_id), ships its 128 bytes to every
-// rank out of band (MPI, a socket, a file), every rank creates the
-// communicator on its ctx's device (ba_comm_create), then each call resolves
-// this rank's contiguous, word-aligned share of the trial index space and
-// all-reduces the 16 run counters over RCCL (xGMI on one node).  No trial data
-// crosses GPUs: every draw is keyed by the global trial index, so the shares
-// give the same counters as one unsharded run.
+// ba_multi.cpp -- the multi-GPU layer inside the C ABI (SURVEY.md §8b/§8e:
+// the library owns the RCCL communicators).  One process per GPU: rank 0 makes
+// a unique id (ba_comm_unique_id), ships its 128 bytes to every rank out of
+// band (MPI, a socket, a file, torch.distributed's store), every rank creates
+// the communicator on its ctx's device (ba_comm_create).  Two ways the path
+// shards, each with exactly the exchange it needs:
+//
+//  * trial data-parallel (ba_run_trials_multi, or per-batch runs plus
+//    ba_comm_allreduce_device): each rank resolves a contiguous word-aligned
+//    share of the trial index space; every draw is keyed by the global trial
+//    index, so the shares give the same counters as one unsharded run.  The
+//    only collective is an all-reduce of the 16 run counters.
+//  * one huge instance split by first-hop subtree (ba_run_instance_split_multi,
+//    or ba_subtree_votes_device + ba_comm_allgather_votes_device +
+//    ba_root_from_votes_device): rank r owns the first hops ba_subtree_share
+//    gives it, computes their level-1 child results in place in the full vote
+//    array, and the ranks exchange them with one grouped broadcast per rank
+//    (an all-gather of unequal shares, no padding or reassembly); every rank
+//    then finishes the root majorities and quorum (ba.py:159-255).
+//
+// Error agreement: a rank whose local work fails still takes part in every
+// collective of the call and raises an error flag that is all-reduced with
+// the counters, so no rank blocks in a collective another rank skipped and
+// every rank returns the error.
 //
 // RCCL is opened with dlopen on first use: torch's wheel bundles its own
 // librccl.so, and a process that imports torch keeps that copy (RTLD_NOLOAD
@@ -23,6 +37,7 @@
 #include "../../include/ba.h"
 
 extern "C" int ba_fail_internal(int code, const char* msg);  // ba_api.cpp: sets ba_last_error
+extern "C" int ba_validate_internal(const ba_params* p, uint64_t batch);  // ba_api.cpp
 
 namespace {
 
@@ -33,6 +48,9 @@ struct Rccl {
     decltype(&ncclCommInitRank) comm_init_rank = nullptr;
     decltype(&ncclCommDestroy) comm_destroy = nullptr;
     decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclBroadcast) broadcast = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
 };
 
@@ -50,9 +68,12 @@ Rccl& rccl() {
     r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(r.h, "ncclCommInitRank");
     r.comm_destroy = (decltype(r.comm_destroy))dlsym(r.h, "ncclCommDestroy");
     r.all_reduce = (decltype(r.all_reduce))dlsym(r.h, "ncclAllReduce");
+    r.broadcast = (decltype(r.broadcast))dlsym(r.h, "ncclBroadcast");
+    r.group_start = (decltype(r.group_start))dlsym(r.h, "ncclGroupStart");
+    r.group_end = (decltype(r.group_end))dlsym(r.h, "ncclGroupEnd");
     r.error_string = (decltype(r.error_string))dlsym(r.h, "ncclGetErrorString");
-    if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.all_reduce ||
-        !r.error_string)
+    if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.all_reduce || !r.broadcast ||
+        !r.group_start || !r.group_end || !r.error_string)
         r.h = nullptr;
     return r;
 }
@@ -66,12 +87,16 @@ int failf(int code, const char* fmt, ...) {
     return ba_fail_internal(code, buf);
 }
 
+constexpr int kErrSlot = BA_NCOUNTERS - 1;  // error flag, all-reduced with the counters
+
 }  // namespace
 
 struct ba_comm {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0, device = 0;
     uint64_t* d_cnt = nullptr;  // BA_NCOUNTERS uint64 on the device, all-reduced in place
+    uint64_t* d_votes = nullptr;  // full vote array of the split (grown on demand)
+    size_t votes_bytes = 0;
     hipStream_t stream = nullptr;
 };
 
@@ -129,9 +154,20 @@ extern "C" void ba_comm_destroy(struct ba_comm* c) {
     if (c->comm && rccl().h) (void)rccl().comm_destroy(c->comm);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->d_cnt) (void)hipFree(c->d_cnt);
+    if (c->d_votes) (void)hipFree(c->d_votes);
     delete c;
 }
 
+extern "C" int ba_comm_rank(struct ba_comm* comm, int* nranks, int* rank) {
+    if (!comm) return failf(BA_EINVAL, "comm is NULL");
+    if (nranks) *nranks = comm->nranks;
+    if (rank) *rank = comm->rank;
+    return BA_OK;
+}
+
+// ---------------------------------------------------------------------------
+// partition arithmetic (host only)
+// ---------------------------------------------------------------------------
 extern "C" int ba_trial_share(uint64_t total_trials, int nranks, int rank, uint64_t* first,
                               uint64_t* count) {
     if (nranks < 1 || rank < 0 || rank >= nranks || !first || !count)
@@ -145,39 +181,164 @@ extern "C" int ba_trial_share(uint64_t total_trials, int nranks, int rank, uint6
     return BA_OK;
 }
 
+extern "C" int ba_subtree_share(uint32_t n, int nranks, int rank, uint32_t* j_begin,
+                                uint32_t* j_end) {
+    if (n < 3 || n > BA_MAX_GENERALS || nranks < 1 || rank < 0 || rank >= nranks || !j_begin ||
+        !j_end)
+        return failf(BA_EINVAL, "n=%u, rank %d of %d ranks", n, rank, nranks);
+    const uint64_t L = n - 1;  // first-hop lieutenants; ranks beyond L get empty shares
+    *j_begin = (uint32_t)(L * (uint64_t)rank / (uint64_t)nranks);
+    *j_end = (uint32_t)(L * (uint64_t)(rank + 1) / (uint64_t)nranks);
+    return BA_OK;
+}
+
+// ---------------------------------------------------------------------------
+// collectives (asynchronous on `stream`)
+// ---------------------------------------------------------------------------
+extern "C" int ba_comm_allreduce_device(struct ba_comm* comm, uint64_t* d_counters, void* stream) {
+    if (!comm || !d_counters) return failf(BA_EINVAL, "comm and d_counters are required");
+    if (hipSetDevice(comm->device) != hipSuccess) return failf(BA_EDEVICE, "hipSetDevice");
+    Rccl& r = rccl();
+    const ncclResult_t e = r.all_reduce(d_counters, d_counters, BA_NCOUNTERS, ncclUint64, ncclSum,
+                                        comm->comm, (hipStream_t)stream);
+    if (e != ncclSuccess) return failf(BA_EDEVICE, "ncclAllReduce: %s", r.error_string(e));
+    return BA_OK;
+}
+
+extern "C" int ba_comm_allgather_votes_device(struct ba_comm* comm, uint32_t n, uint32_t m,
+                                              uint64_t batch, uint64_t* d_votes, void* stream) {
+    if (!comm || !d_votes) return failf(BA_EINVAL, "comm and d_votes are required");
+    if (ba_vote_slots(n, m, 0, n >= 2 ? n - 1 : 0) == 0)
+        return failf(BA_EINVAL, "no first-hop votes for n=%u, m=%u", n, m);
+    if (hipSetDevice(comm->device) != hipSuccess) return failf(BA_EDEVICE, "hipSetDevice");
+    const uint64_t W = (batch + 63) / 64, row = (uint64_t)(n - 2) * W;
+    Rccl& r = rccl();
+    ncclResult_t e = r.group_start();
+    for (int q = 0; q < comm->nranks && e == ncclSuccess; ++q) {
+        uint32_t jb = 0, je = 0;
+        (void)ba_subtree_share(n, comm->nranks, q, &jb, &je);
+        if (je == jb) continue;
+        uint64_t* part = d_votes + (uint64_t)jb * row;  // rank q's rows, in place on every rank
+        e = r.broadcast(part, part, (size_t)(je - jb) * row, ncclUint64, q, comm->comm,
+                        (hipStream_t)stream);
+    }
+    const ncclResult_t e2 = r.group_end();
+    if (e != ncclSuccess || e2 != ncclSuccess)
+        return failf(BA_EDEVICE, "vote all-gather (grouped ncclBroadcast): %s",
+                     r.error_string(e != ncclSuccess ? e : e2));
+    return BA_OK;
+}
+
+// ---------------------------------------------------------------------------
+// blocking whole-job entry points
+// ---------------------------------------------------------------------------
+// Sum every rank's error flag -- and, for trial-DP, the counters (a split
+// computes the same whole-job counters on every rank) -- over the ranks, copy
+// them to the host and report: the local error, else "another rank failed",
+// else OK.
+static int finish_job(ba_comm* comm, int local_rc, ba_counters* counters_out, bool sum_counters) {
+    if (local_rc != BA_OK) {
+        static const uint64_t one = 1;
+        (void)hipMemcpyAsync(comm->d_cnt + kErrSlot, &one, sizeof one, hipMemcpyHostToDevice,
+                             comm->stream);
+    }
+    ba_counters tmp;
+    int rc = BA_OK;
+    if (sum_counters) {
+        rc = ba_comm_allreduce_device(comm, comm->d_cnt, comm->stream);
+    } else {
+        Rccl& r = rccl();
+        const ncclResult_t e = r.all_reduce(comm->d_cnt + kErrSlot, comm->d_cnt + kErrSlot, 1,
+                                            ncclUint64, ncclSum, comm->comm, comm->stream);
+        if (e != ncclSuccess) rc = failf(BA_EDEVICE, "ncclAllReduce: %s", r.error_string(e));
+    }
+    if (hipMemcpyAsync(tmp.v, comm->d_cnt, sizeof tmp.v, hipMemcpyDeviceToHost, comm->stream) !=
+            hipSuccess ||
+        hipStreamSynchronize(comm->stream) != hipSuccess)
+        rc = failf(BA_EDEVICE, "counter read-back");
+    if (local_rc != BA_OK) return local_rc;
+    if (rc != BA_OK) return rc;
+    if (tmp.v[kErrSlot] != 0)
+        return failf(BA_EDEVICE, "%llu other rank(s) failed this call",
+                     (unsigned long long)tmp.v[kErrSlot]);
+    tmp.v[kErrSlot] = 0;
+    if (counters_out) *counters_out = tmp;
+    return BA_OK;
+}
+
+static int begin_job(ba_comm* comm) {
+    if (hipSetDevice(comm->device) != hipSuccess) return failf(BA_EDEVICE, "hipSetDevice");
+    if (hipMemsetAsync(comm->d_cnt, 0, BA_NCOUNTERS * sizeof(uint64_t), comm->stream) != hipSuccess)
+        return failf(BA_EDEVICE, "hipMemsetAsync");
+    return BA_OK;
+}
+
 extern "C" int ba_run_trials_multi(struct ba_ctx* ctx, struct ba_comm* comm, const ba_params* p,
                                    uint64_t total_trials, uint64_t* d_decisions,
                                    uint8_t* d_outcome, ba_counters* counters_out,
                                    uint64_t* share_first, uint64_t* share_count) {
     if (!ctx || !comm || !p) return failf(BA_EINVAL, "ctx, comm and params are required");
-    if (p->faulty_mode == BA_FAULTY_GIVEN || p->order_mode == BA_ORDER_GIVEN ||
-        p->lie_mode == BA_LIE_TABLE)
-        return failf(BA_EINVAL, "ba_run_trials_multi draws its inputs (faulty/order modes other "
-                     "than GIVEN, Philox lies); shard given inputs with ba_run_trials_device");
-    if (p->first_trial % 64 != 0) return failf(BA_EINVAL, "first_trial must be a multiple of 64");
     uint64_t first = 0, count = 0;
     int rc = ba_trial_share(total_trials, comm->nranks, comm->rank, &first, &count);
     if (rc != BA_OK) return rc;
     if (share_first) *share_first = first;
     if (share_count) *share_count = count;
-    if (hipSetDevice(comm->device) != hipSuccess) return failf(BA_EDEVICE, "hipSetDevice");
-    if (hipMemsetAsync(comm->d_cnt, 0, BA_NCOUNTERS * sizeof(uint64_t), comm->stream) != hipSuccess)
-        return failf(BA_EDEVICE, "hipMemsetAsync");
-    ba_params q = *p;
-    q.first_trial = p->first_trial + first;  // draws keyed by the global trial index
-    if (count > 0 &&
-        (rc = ba_run_trials_device(ctx, &q, count, nullptr, nullptr, nullptr, nullptr, d_decisions,
-                                   d_outcome, comm->d_cnt, comm->stream)) != BA_OK)
-        return rc;
-    // the only collective: the run counters, summed over ranks in place
-    Rccl& r = rccl();
-    const ncclResult_t e = r.all_reduce(comm->d_cnt, comm->d_cnt, BA_NCOUNTERS, ncclUint64,
-                                        ncclSum, comm->comm, comm->stream);
-    if (e != ncclSuccess) return failf(BA_EDEVICE, "ncclAllReduce: %s", r.error_string(e));
-    if (counters_out &&
-        hipMemcpyAsync(counters_out->v, comm->d_cnt, BA_NCOUNTERS * sizeof(uint64_t),
-                       hipMemcpyDeviceToHost, comm->stream) != hipSuccess)
-        return failf(BA_EDEVICE, "counter copy");
-    if (hipStreamSynchronize(comm->stream) != hipSuccess) return failf(BA_EDEVICE, "sync");
-    return BA_OK;
+    if ((rc = begin_job(comm)) != BA_OK) return rc;  // this rank cannot reach its device
+    // every rank validates before any collective; a failure still joins the all-reduce
+    int local = ba_validate_internal(p, total_trials);
+    if (local == BA_OK && (p->faulty_mode == BA_FAULTY_GIVEN || p->order_mode == BA_ORDER_GIVEN ||
+                           p->lie_mode == BA_LIE_TABLE))
+        local = failf(BA_EINVAL, "ba_run_trials_multi draws its inputs (faulty/order modes other "
+                      "than GIVEN, Philox lies); shard given inputs with ba_run_trials_device");
+    if (local == BA_OK && count > 0) {
+        ba_params q = *p;
+        q.first_trial = p->first_trial + first;  // draws keyed by the global trial index
+        local = ba_run_trials_device(ctx, &q, count, nullptr, nullptr, nullptr, nullptr, d_decisions,
+                                     d_outcome, comm->d_cnt, comm->stream);
+    }
+    return finish_job(comm, local, counters_out, true);
+}
+
+extern "C" int ba_run_instance_split_multi(struct ba_ctx* ctx, struct ba_comm* comm,
+                                           const ba_params* p, uint64_t batch,
+                                           const uint32_t* d_faulty_mask, const uint8_t* d_order,
+                                           uint64_t* d_decisions, uint8_t* d_outcome,
+                                           ba_counters* counters_out) {
+    if (!ctx || !comm || !p) return failf(BA_EINVAL, "ctx, comm and params are required");
+    int rc = begin_job(comm);
+    if (rc != BA_OK) return rc;
+    int local = ba_validate_internal(p, batch);
+    const uint32_t n = p->n;
+    const uint64_t slots = local == BA_OK ? ba_vote_slots(n, p->m, 0, n - 1) : 0;
+    if (local == BA_OK && slots == 0)
+        local = failf(BA_ENOTSUP, "OM(0) has no relay subtrees (n=%u, m=%u)", n, p->m);
+    const uint64_t W = (batch + 63) / 64;
+    const size_t need = (size_t)(slots * W * sizeof(uint64_t));
+    if (local == BA_OK && need > comm->votes_bytes) {
+        (void)hipStreamSynchronize(comm->stream);
+        if (comm->d_votes) (void)hipFree(comm->d_votes);
+        comm->d_votes = nullptr;
+        comm->votes_bytes = 0;
+        if (hipMalloc(&comm->d_votes, need) != hipSuccess)
+            local = failf(BA_ENOMEM, "vote buffer (%zu B)", need);
+        else
+            comm->votes_bytes = need;
+    }
+    if (local == BA_OK && batch > 0) {
+        uint32_t jb = 0, je = 0;
+        (void)ba_subtree_share(n, comm->nranks, comm->rank, &jb, &je);
+        if (je > jb)
+            local = ba_subtree_votes_device(ctx, p, batch, jb, je, d_faulty_mask, d_order,
+                                            comm->d_votes + (uint64_t)jb * (n - 2) * W,
+                                            comm->stream);
+    }
+    // the exchange runs whatever happened locally (no rank may skip a collective)
+    if (slots > 0 && batch > 0) {
+        const int e = ba_comm_allgather_votes_device(comm, n, p->m, batch, comm->d_votes, comm->stream);
+        if (local == BA_OK) local = e;
+    }
+    if (local == BA_OK && batch > 0)
+        local = ba_root_from_votes_device(ctx, p, batch, d_faulty_mask, d_order, comm->d_votes,
+                                          d_decisions, d_outcome, comm->d_cnt, comm->stream);
+    return finish_job(comm, local, counters_out, false);
 }

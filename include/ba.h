@@ -16,9 +16,12 @@
  *     take device pointers and a hipStream_t (as void*) and are asynchronous.
  *   - One ctx per host thread; a ctx is not thread-safe.  The library owns
  *     the device scratch it allocates inside the ctx (including the run
- *     counter reduction slots), so the *_device calls of one ctx must be
- *     stream-ordered: do not let two of them run concurrently on different
- *     streams (use one ctx per concurrent stream).
+ *     counter reduction slots).  Calls of one ctx may be made on different
+ *     streams: the library orders each call after the ctx's previous one
+ *     (an event on the previous call's stream), except while the stream is
+ *     capturing a graph -- a graph replay's ordering is the caller's.  Device
+ *     buffers a captured graph holds stay valid until the ctx grows its
+ *     scratch for a LARGER call: give a graph its own ctx.
  *
  * General indexing: the live generals sorted by id are
  * indexed 0..n-1; index 0 is the commander (lowest live id, ba.py:381 +
@@ -200,21 +203,15 @@ int ba_root_from_votes_device(struct ba_ctx* ctx, const ba_params* p, uint64_t b
                               const uint64_t* d_votes, uint64_t* d_decisions, uint8_t* d_outcome,
                               uint64_t* d_counters, void* stream);
 
-/* ---- multi-GPU trial data-parallel runs (no ba.py analogue:
- * its generals are threads of one process) ---------------------------------
+/* ---- multi-GPU (no ba.py analogue: its generals are threads of
+ * one process, ba.py:104-112) ----------------------------------------------
  * One process per GPU.  Rank 0 calls ba_comm_unique_id and ships the
- * BA_COMM_ID_BYTES bytes to every rank out of band (MPI, a socket, a file);
- * every rank calls ba_comm_create on its ctx (which owns the RCCL communicator,
- * a counter buffer and a stream).  ba_run_trials_multi resolves this rank's
- * contiguous, 64-trial-word-aligned share (ba_trial_share) of the trials
- * [p->first_trial, p->first_trial + total_trials) -- inputs drawn on the device
- * (faulty/order modes other than GIVEN), Philox lies, every draw keyed by the
- * global trial index -- writes this share's decisions / outcome bytes to the
- * optional device buffers (share_count entries), and all-reduces the run
- * counters over RCCL: counters_out holds the whole job's totals on every rank,
- * equal to one unsharded ba_run_trials.  Blocking (returns after the
- * all-reduce).  RCCL is opened at run time (librccl.so.1, or the copy already
- * loaded in the process). */
+ * BA_COMM_ID_BYTES bytes to every rank out of band (MPI, a socket, a file, a
+ * torch.distributed store); every rank calls ba_comm_create on its ctx (the
+ * communicator owns an RCCL communicator, a counter buffer, a vote buffer and
+ * a stream).  RCCL is opened at run time (librccl.so.1, or the copy already
+ * loaded in the process).  Every rank of a comm must make the same sequence
+ * of collective calls with the same params. */
 #define BA_COMM_ID_BYTES 128
 struct ba_comm;
 int ba_ctx_device(struct ba_ctx* ctx, int* device);
@@ -222,12 +219,52 @@ int ba_comm_unique_id(unsigned char id[BA_COMM_ID_BYTES]);
 int ba_comm_create(struct ba_ctx* ctx, int nranks, int rank,
                    const unsigned char id[BA_COMM_ID_BYTES], struct ba_comm** out);
 void ba_comm_destroy(struct ba_comm* comm);
+int ba_comm_rank(struct ba_comm* comm, int* nranks, int* rank);
+
+/* Partition arithmetic (host only).  ba_trial_share: rank's contiguous,
+ * 64-trial-word-aligned share [first, first + count) of total_trials, words
+ * split as evenly as possible.  ba_subtree_share: rank's first-hop lieutenant
+ * range [j_begin, j_end) of the n-1 subtrees (15 over 8 ranks: 1,2,2,2,2,2,2,2;
+ * ranks beyond n-1 get empty ranges). */
 int ba_trial_share(uint64_t total_trials, int nranks, int rank, uint64_t* first,
                    uint64_t* count);
+int ba_subtree_share(uint32_t n, int nranks, int rank, uint32_t* j_begin, uint32_t* j_end);
+
+/* Collectives, asynchronous on `stream` (a hipStream_t as void*).
+ * ba_comm_allreduce_device: d_counters (BA_NCOUNTERS uint64) summed over the
+ * ranks in place -- the only exchange trial-DP needs.
+ * ba_comm_allgather_votes_device: d_votes is the full [(n-1)(n-2)][W] vote
+ * array of ba_subtree_votes_device (W = ceil(batch/64)) in which every rank
+ * has written the rows of its ba_subtree_share; afterwards every rank holds
+ * every row (one grouped RCCL broadcast per rank: an all-gather of unequal
+ * shares in place, no padding). */
+int ba_comm_allreduce_device(struct ba_comm* comm, uint64_t* d_counters, void* stream);
+int ba_comm_allgather_votes_device(struct ba_comm* comm, uint32_t n, uint32_t m, uint64_t batch,
+                                   uint64_t* d_votes, void* stream);
+
+/* Whole jobs, blocking (they return after the collectives, on the comm's
+ * stream).  A rank whose local work fails still joins every collective and
+ * raises an error flag all-reduced with the counters: every rank then returns
+ * an error, none blocks.
+ * ba_run_trials_multi: trial-DP over [p->first_trial, + total_trials) --
+ *   inputs drawn on the device (faulty/order modes other than GIVEN), Philox
+ *   lies, every draw keyed by the global trial index; this rank's share of the
+ *   decisions / outcome bytes goes to the optional device buffers
+ *   (share_count entries); counters_out = the whole job's totals on every
+ *   rank, equal to one unsharded ba_run_trials.
+ * ba_run_instance_split_multi: `batch` (normally few, huge) instances split by
+ *   first-hop subtree -- subtree votes, vote all-gather, root majorities and
+ *   quorum; decisions / outcome (batch entries) and counters_out identical on
+ *   every rank and equal to an unsplit ba_run_trials on the same params
+ *   (LEVELS engine, Philox lies, given or drawn inputs). */
 int ba_run_trials_multi(struct ba_ctx* ctx, struct ba_comm* comm, const ba_params* p,
                         uint64_t total_trials, uint64_t* d_decisions, uint8_t* d_outcome,
                         ba_counters* counters_out, uint64_t* share_first,
                         uint64_t* share_count);
+int ba_run_instance_split_multi(struct ba_ctx* ctx, struct ba_comm* comm, const ba_params* p,
+                                uint64_t batch, const uint32_t* d_faulty_mask,
+                                const uint8_t* d_order, uint64_t* d_decisions,
+                                uint8_t* d_outcome, ba_counters* counters_out);
 
 /* Per-kernel timing (tracing aux subsystem; replaces nothing in ba.py, which
  * only prints).  When enabled, every kernel the ctx launches is bracketed by

@@ -1,10 +1,10 @@
-"""Multi-GPU layer (ba_amd.dist) on CPU with gloo, world sizes 2 and 3.
-
-The device work is done by a stand-in backend that answers from the C oracle
-(test infrastructure), so these tests pin the host logic: word-aligned trial
-shards, the counter all-reduce, the first-hop subtree partition, vote padding,
-the all-gather and the reassembly order.  The GPU tests at the bottom run the
-real libba_hip split entry points."""
+"""Multi-GPU layer: the C ABI's sharding (ba_trial_share, ba_subtree_share),
+the torch.distributed rendezvous of ba_amd.dist, and -- on CPU with gloo,
+world sizes 2, 3 and 8 -- the composition of the shards the library's
+collectives perform (counter all-reduce, vote all-gather), with the C oracle
+doing each rank's device work and gloo standing in for RCCL.  The GPU tests at
+the bottom run the real libba_hip entries over a one-rank RCCL communicator
+(RCCL refuses two ranks on one GPU; N>1 runs on the driver's 8-GPU node)."""
 import os
 import socket
 
@@ -17,35 +17,6 @@ import torch.multiprocessing as mp
 import oracle_c
 
 COUNTERS = 12
-
-
-class OracleBackend:
-    device = torch.device("cpu")
-
-    def counters(self):
-        return torch.zeros(16, dtype=torch.int64)
-
-    def run_trials(self, p, batch, counters, decisions=None, outcome=None):
-        _, _, c = oracle_c.run(p.n, p.m, batch, seed=p.seed, faulty_mode=p.faulty_mode, f=p.f,
-                               order_mode=p.order_mode, order_value=p.order_value,
-                               first_trial=p.first_trial)
-        counters[:COUNTERS] += torch.tensor(list(c.values()), dtype=torch.int64)
-
-    def _kw(self, p):
-        return dict(seed=p.seed, faulty_mode=p.faulty_mode, f=p.f, order_mode=p.order_mode,
-                    order_value=p.order_value, first_trial=p.first_trial)
-
-    def subtree_votes(self, p, batch, jb, je):
-        v = oracle_c.votes(p.n, p.m, batch, **self._kw(p))
-        return torch.from_numpy(oracle_c.pack_votes(v, jb, je).view(np.int64).copy())
-
-    def root_from_votes(self, p, batch, votes):
-        want = oracle_c.pack_votes(oracle_c.votes(p.n, p.m, batch, **self._kw(p)))
-        assert np.array_equal(votes.numpy().view(np.uint64), want), "gathered votes misassembled"
-        dec, out, c = oracle_c.run(p.n, p.m, batch, **self._kw(p))
-        cnt = self.counters()
-        cnt[:COUNTERS] = torch.tensor(list(c.values()), dtype=torch.int64)
-        return torch.from_numpy(dec.view(np.int64)), torch.from_numpy(out), cnt
 
 
 def _free_port():
@@ -70,35 +41,76 @@ def spawn(fn, world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, fn, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in procs)
+    res = dict(q.get(timeout=180) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     return [res[r] for r in range(world)]
 
 
-def test_word_shard_partitions():
-    from ba_amd.dist import subtree_ranges, word_shard
-    for total in (0, 1, 63, 64, 65, 1000, 64 * 1001 + 3):
+# --- partition arithmetic of the C ABI (host-only entries, no device) -------------
+def test_trial_share_partitions():
+    from ba_amd import lib as L
+    for total in (0, 1, 63, 64, 65, 1000, 64 * 1001 + 3, 64 << 20):
         for world in (1, 2, 3, 8):
-            parts = [word_shard(total, r, world) for r in range(world)]
+            parts = [L.trial_share(total, world, r) for r in range(world)]
             pos = 0
             for first, count in parts:
                 assert first % 64 == 0 and (count == 0 or first == pos)
                 pos = first + count if count else pos
             assert sum(c for _, c in parts) == total
-    assert subtree_ranges(15, 8) == [(0, 1), (1, 3), (3, 5), (5, 7), (7, 9), (9, 11), (11, 13),
-                                     (13, 15)]
-    assert subtree_ranges(3, 4)[0] == (0, 0)  # more ranks than subtrees: idle ranks
+            words = [(c + 63) // 64 for _, c in parts]
+            assert max(words) - min(words) <= 1  # balanced to one word
 
 
-def _dp(rank, world):
+def test_subtree_share_partitions():
     from ba_amd import dist as D
-    cnt = D.run_trials_dp(OracleBackend(), 10, 3, 64 * 37 + 11, seed=5, f=3, chunk=64 * 5)
-    return cnt[:COUNTERS].tolist()
+    from ba_amd import lib as L
+    for n in (3, 4, 10, 13, 16, 32):
+        for world in (1, 2, 3, 8, 40):
+            ranges = [L.subtree_share(n, world, r) for r in range(world)]
+            assert ranges[0][0] == 0 and ranges[-1][1] == n - 1
+            for (a, b), (c, d) in zip(ranges, ranges[1:]):
+                assert b == c and a <= b  # contiguous, in rank order
+            sizes = [b - a for a, b in ranges]
+            assert max(sizes) - min(sizes) <= 1
+    assert D.subtree_ranges(15, 8) == [(0, 1), (1, 3), (3, 5), (5, 7), (7, 9), (9, 11), (11, 13),
+                                       (13, 15)]
+    assert L.subtree_share(4, 4, 0) == (0, 0)  # more ranks than subtrees: idle ranks
+    with pytest.raises(L.BAError):
+        L.subtree_share(2, 1, 0)
+
+
+# --- gloo rehearsals of the collectives' composition ------------------------------
+def _rendezvous(rank, world):
+    from ba_amd import dist as D
+    return D.rendezvous_uid()
 
 
 @pytest.mark.parametrize("world", [2, 3])
+def test_rendezvous_delivers_rank0_uid(world):
+    """ba_amd.dist.rendezvous_uid: RCCL's unique id (ncclGetUniqueId works without a
+    GPU) made on rank 0 reaches every rank byte for byte."""
+    got = spawn(_rendezvous, world)
+    assert all(len(u) == 128 and u == got[0] for u in got)
+
+
+def _dp(rank, world):
+    """Each rank resolves its ba_trial_share with the oracle; gloo sums the
+    counters as ba_comm_allreduce_device does."""
+    from ba_amd import lib as L
+    total = 64 * 37 + 11
+    first, count = L.trial_share(total, world, rank)
+    cnt = torch.zeros(16, dtype=torch.int64)
+    if count:
+        _, _, c = oracle_c.run(10, 3, count, seed=5, faulty_mode=1, f=3, order_mode=1,
+                               first_trial=first)
+        cnt[:COUNTERS] = torch.tensor(list(c.values()), dtype=torch.int64)
+    dist.all_reduce(cnt)
+    return cnt[:COUNTERS].tolist()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_trial_dp_counters_allreduced(world):
     got = spawn(_dp, world)
     _, _, want = oracle_c.run(10, 3, 64 * 37 + 11, seed=5, faulty_mode=1, f=3, order_mode=1)
@@ -107,23 +119,31 @@ def test_trial_dp_counters_allreduced(world):
 
 
 def _split(rank, world):
-    from ba_amd import dist as D
+    """Each rank computes the vote rows of its ba_subtree_share (oracle votes in the
+    library's layout), the rows are exchanged (gloo all-gather in place of the
+    grouped broadcast), and the assembled array must equal the whole instance's."""
     from ba_amd import lib as L
-    p = L.make_params(10, 3, seed=9, faulty_mode=L.FAULTY_RANDOM, f=4, order_mode=L.ORDER_RANDOM,
-                      first_trial=128)
-    dec, out, cnt = D.run_instance_split(OracleBackend(), p, 70)
-    return dec.tolist(), out.tolist(), cnt[:COUNTERS].tolist()
+    n, m, B = 10, 3, 70
+    kw = dict(seed=9, faulty_mode=1, f=4, order_mode=1, first_trial=128)
+    jb, je = L.subtree_share(n, world, rank)
+    v = oracle_c.votes(n, m, B, **kw)
+    mine = oracle_c.pack_votes(v, jb, je) if je > jb else np.zeros((0, (B + 63) // 64), np.uint64)
+    parts = [None] * world
+    dist.all_gather_object(parts, (jb, je, mine.tobytes()))
+    W = (B + 63) // 64
+    full = np.zeros(((n - 1) * (n - 2), W), np.uint64)
+    for a, b, raw in parts:
+        if b > a:
+            full[a * (n - 2):b * (n - 2)] = np.frombuffer(raw, np.uint64).reshape(-1, W)
+    return full.tobytes()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_instance_split_gathers_votes(world):
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_instance_split_assembles_votes(world):
     got = spawn(_split, world)
-    dec, out, c = oracle_c.run(10, 3, 70, seed=9, faulty_mode=1, f=4, order_mode=1,
-                               first_trial=128)
-    for r in range(world):
-        assert got[r][0] == dec.view(np.int64).tolist()
-        assert got[r][1] == out.tolist()
-        assert got[r][2] == list(c.values())
+    v = oracle_c.votes(10, 3, 70, seed=9, faulty_mode=1, f=4, order_mode=1, first_trial=128)
+    want = oracle_c.pack_votes(v).tobytes()
+    assert all(g == want for g in got)
 
 
 def test_oracle_votes_reproduce_root_decisions():
@@ -145,30 +165,37 @@ def test_oracle_votes_reproduce_root_decisions():
             assert (int(dec[t]) >> (2 * r)) & 3 == code
 
 
+# --- GPU: the real entries ---------------------------------------------------------
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,m,B,nr", [(10, 3, 200, 4), (7, 1, 100, 4), (9, 2, 130, 4), (16, 5, 2, 4),
                                       # odd n at depth 3: a first-hop subtree holds an odd
                                       # number of level-1 slots, so with 3 ranks a range
                                       # starts mid slot pair (k_relay_top's range edges)
-                                      (9, 3, 150, 3), (5, 3, 70, 3), (13, 3, 65, 5)])
+                                      (9, 3, 150, 3), (5, 3, 70, 3), (13, 3, 65, 5),
+                                      (16, 5, 70, 8)])
 def test_subtree_votes_match_oracle_gpu(engine, n, m, B, nr):
-    from ba_amd import dist as D
+    """Every rank's ba_subtree_votes_device rows (ranges from ba_subtree_share) equal
+    the oracle's, and the root pass over the assembled rows equals the oracle's run."""
     from ba_amd import lib as L
     dev = torch.device("cuda", 0)
-    be = D.DeviceBackend(engine, dev)
     kw = dict(seed=11, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1, order_mode=L.ORDER_RANDOM,
               first_trial=64 * 3)
-    p = L.make_params(n, m, **{k: v for k, v in kw.items()})
+    p = L.make_params(n, m, **kw)
+    W = (B + 63) // 64
     v_or = oracle_c.votes(n, m, B, **kw)
-    ranges = D.subtree_ranges(n - 1, nr)
-    parts = []
-    for jb, je in ranges:
+    full = torch.zeros(((n - 1) * (n - 2), W), dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    for r in range(nr):
+        jb, je = L.subtree_share(n, nr, r)
         if je > jb:
-            got = be.subtree_votes(p, B, jb, je).cpu().numpy().view(np.uint64)
+            engine.subtree_votes_device(p, B, jb, je, full[jb * (n - 2):].data_ptr(), stream=s)
+            got = full[jb * (n - 2):je * (n - 2)].cpu().numpy().view(np.uint64)
             assert np.array_equal(got, oracle_c.pack_votes(v_or, jb, je)), (jb, je)
-            parts.append(got)
-    full = torch.from_numpy(np.concatenate(parts).view(np.int64)).to(dev)
-    dec, out, cnt = be.root_from_votes(p, B, full)
+    dec = torch.empty(B, dtype=torch.int64, device=dev)
+    out = torch.empty(B, dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(16, dtype=torch.int64, device=dev)
+    engine.root_from_votes_device(p, B, full.data_ptr(), cnt.data_ptr(), d_decisions=dec.data_ptr(),
+                                  d_outcome=out.data_ptr(), stream=s)
     torch.cuda.synchronize()
     od, oo, oc = oracle_c.run(n, m, B, **kw)
     assert np.array_equal(dec.cpu().numpy().view(np.uint64), od)
@@ -177,23 +204,54 @@ def test_subtree_votes_match_oracle_gpu(engine, n, m, B, nr):
 
 
 @pytest.mark.gpu
-def test_split_equals_unsplit_n16_m5_gpu(engine):
-    """Config 5: one batch of n=16, m=5 instances through run_instance_split
-    (world 1) equals ba_run_trials on the same params."""
+def test_split_multi_world1_equals_unsplit_n16_m5(engine):
+    """Config 5 through ba_run_instance_split_multi (one-rank RCCL communicator: the
+    grouped broadcast runs, with one root) equals ba_run_trials on the same params,
+    and equals the C port on the full 1024-instance batch."""
     from ba_amd import dist as D
     from ba_amd import lib as L
     dev = torch.device("cuda", 0)
-    be = D.DeviceBackend(engine, dev)
-    p = L.make_params(16, 5, seed=0xBA5EED, faulty_mode=L.FAULTY_RANDOM, f=5,
-                      order_mode=L.ORDER_RANDOM)
-    B = 300
-    dec, out, cnt = D.run_instance_split(be, p, B)
-    ref = engine.run(16, 5, B, seed=0xBA5EED, faulty_mode=L.FAULTY_RANDOM, f=5,
-                     order_mode=L.ORDER_RANDOM, engine=L.ENGINE_LEVELS)
-    torch.cuda.synchronize()
-    assert np.array_equal(dec.cpu().numpy().view(np.uint64), ref.decisions)
-    assert np.array_equal(out.cpu().numpy(), ref.outcome)
-    assert cnt.cpu().tolist()[:COUNTERS] == [ref.counters[k] for k in L.COUNTER_NAMES]
+    comm = L.Comm(engine, 1, 0, L.comm_unique_id())
+    try:
+        p = L.make_params(16, 5, seed=0xBA5EED, faulty_mode=L.FAULTY_RANDOM, f=5,
+                          order_mode=L.ORDER_RANDOM)
+        B = 1024
+        dec, out, cnt = D.run_instance_split(comm, p, B, dev)
+        ref = engine.run(16, 5, B, seed=0xBA5EED, faulty_mode=L.FAULTY_RANDOM, f=5,
+                         order_mode=L.ORDER_RANDOM, engine=L.ENGINE_LEVELS)
+        assert np.array_equal(dec.cpu().numpy().view(np.uint64), ref.decisions)
+        assert np.array_equal(out.cpu().numpy(), ref.outcome)
+        assert cnt == ref.counters
+        od, oo, oc = oracle_c.sliced_run(16, 5, B, seed=0xBA5EED, faulty_mode=1, f=5,
+                                         order_mode=1)
+        assert np.array_equal(ref.decisions, od) and np.array_equal(ref.outcome, oo)
+        assert {k: cnt[k] for k in oc} == oc
+    finally:
+        comm.close()
+
+
+@pytest.mark.gpu
+def test_comm_allreduce_and_split_errors(engine):
+    """ba_comm_allreduce_device over one rank is the identity; a bad split request
+    fails on the rank (after joining the error all-reduce) instead of hanging."""
+    from ba_amd import lib as L
+    comm = L.Comm(engine, 1, 0, L.comm_unique_id())
+    try:
+        x = torch.arange(16, dtype=torch.int64, device="cuda")
+        comm.allreduce_device(x.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert x.cpu().tolist() == list(range(16))
+        p0 = L.make_params(10, 0, seed=1, faulty_mode=L.FAULTY_RANDOM, f=3,
+                           order_mode=L.ORDER_RANDOM)
+        with pytest.raises(L.BAError) as ei:
+            comm.run_instance_split(p0, 64)
+        assert ei.value.code == L.ENOTSUP
+        # the communicator stays usable after a failed call
+        p = L.make_params(10, 3, seed=1, faulty_mode=L.FAULTY_RANDOM, f=3, order_mode=L.ORDER_RANDOM)
+        c = comm.run_instance_split(p, 100)
+        assert c["trials"] == 100
+    finally:
+        comm.close()
 
 
 @pytest.mark.gpu
@@ -216,19 +274,58 @@ def test_split_api_errors(engine):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,m,B", [(16, 5, 300), (10, 3, 1000), (9, 3, 150)])
 def test_instance_split_graphs_equal_eager(engine, n, m, B):
-    """The hipGraph-captured split (InstanceSplitGraphs) replays to the same
-    decisions / outcome bytes / counters as eager run_instance_split, on every
+    """The hipGraph-captured split (InstanceSplitGraphs, its own ctx) replays to the
+    same decisions / outcome bytes / counters as the eager C-ABI split, on every
     replay (the counters are re-zeroed inside the graph)."""
     from ba_amd import dist as D
     from ba_amd import lib as L
     dev = torch.device("cuda", 0)
     p = L.make_params(n, m, seed=0xBA5EED, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3,
                       order_mode=L.ORDER_RANDOM, first_trial=64 * 5)
-    ref_dec, ref_out, ref_cnt = D.run_instance_split(D.DeviceBackend(engine, dev), p, B)
-    g = D.InstanceSplitGraphs(engine, dev, p, B)
-    for _ in range(3):
-        dec, out, cnt = g.replay()
-        torch.cuda.synchronize()
-        assert torch.equal(dec, ref_dec)
-        assert torch.equal(out, ref_out)
-        assert torch.equal(cnt, ref_cnt)
+    comm = L.Comm(engine, 1, 0, L.comm_unique_id())
+    try:
+        ref_dec, ref_out, ref_cnt = D.run_instance_split(comm, p, B, dev)
+    finally:
+        comm.close()
+    g = D.InstanceSplitGraphs(dev, p, B)
+    try:
+        for _ in range(3):
+            dec, out, cnt = g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(dec, ref_dec)
+            assert torch.equal(out, ref_out)
+            assert cnt.cpu().tolist()[:COUNTERS] == [ref_cnt[k] for k in L.COUNTER_NAMES]
+    finally:
+        g.close()
+
+
+@pytest.mark.gpu
+def test_ctx_orders_calls_across_streams(engine):
+    """Calls of one ctx issued back to back on two different streams (no host sync)
+    share its scratch and counter sink safely: the library orders the second call
+    after the first (include/ba.h).  Both results equal the oracle."""
+    from ba_amd import lib as L
+    dev = torch.device("cuda", 0)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    B = 1 << 16
+    jobs = []
+    for seed, s in ((3, s1), (4, s2), (5, s1)):
+        p = L.make_params(16, 5, seed, L.LIE_PHILOX, L.FAULTY_RANDOM, 5, L.ORDER_RANDOM,
+                          L.ATTACK, L.ENGINE_LEVELS, 0) if seed == 4 else \
+            L.make_params(10, 3, seed, L.LIE_PHILOX, L.FAULTY_RANDOM, 3, L.ORDER_RANDOM)
+        b = 64 if seed == 4 else B
+        dec = torch.empty(b, dtype=torch.int64, device=dev)
+        cnt = torch.zeros(16, dtype=torch.int64, device=dev)
+        jobs.append((p, b, s, dec, cnt))
+    torch.cuda.synchronize()
+    outs = []
+    for p, b, s, dec, cnt in jobs:  # back to back, no host sync in between
+        engine.run_device(p, b, d_decisions=dec.data_ptr(), d_counters=cnt.data_ptr(),
+                          stream=s.cuda_stream)
+        outs.append((p.n, p.m, p.seed, b, dec, cnt))
+    torch.cuda.synchronize()
+    for n, m, seed, b, dec, cnt in outs:
+        od, _, oc = oracle_c.sliced_run(n, m, b, seed=seed, faulty_mode=1, f=(5 if n == 16 else 3),
+                                        order_mode=1)
+        assert np.array_equal(dec.cpu().numpy().view(np.uint64), od), seed
+        assert cnt.cpu().tolist()[:COUNTERS] == list(oc.values()), seed

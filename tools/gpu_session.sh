@@ -18,7 +18,7 @@ run() {  # name seconds cmd...
   return $rc
 }
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }  # 1 = ordinary test failure
-BENCH_PMC="$ROOT/bench.py --steps 3 --warmup 1 --no-cpu --no-profile"
+BENCH_PMC="$ROOT/bench.py --steps 3 --warmup 1 --warm-s 0 --no-cpu --no-profile"
 pmc_pass() {  # name counters...
   local name=$1; shift
   (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv \
@@ -27,15 +27,16 @@ pmc_pass() {  # name counters...
 }
 for s in $STAGES; do
   case $s in
-    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
+    tests) run pytest_gpu 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) run bench 600 python -u bench.py --steps 20 --warmup 3 || exit $? ;;
     bench_levels) run bench_levels 600 python -u bench.py --steps 20 --warmup 3 --engine levels --no-cpu || exit $? ;;
     bench_fused) run bench_fused 600 python -u bench.py --steps 20 --warmup 3 --engine fused --no-cpu || exit $? ;;
     philox) run philox 120 ./tools/philox_bench || exit $? ;;
+    lab) run lab 300 ./tools/om3_lab || exit $? ;;
     prof) (cd /tmp && export TMPDIR=/tmp && mkdir -p "$ROOT/gpurun_out/prof" && \
            timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/prof" -o run -- \
-             python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu --no-profile > "$ROOT/gpurun_out/prof.log" 2>&1); rc=$?
+             python3 "$ROOT/bench.py" --steps 10 --warmup 2 --warm-s 0.3 --no-cpu --no-profile > "$ROOT/gpurun_out/prof.log" 2>&1); rc=$?
           echo "prof rc=$rc" | tee -a gpurun_out/steps.log; tail -3 gpurun_out/prof.log; [ $rc -eq 0 ] || exit $rc ;;
     pmc) pmc_pass sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY || exit $?
          pmc_pass fetch FETCH_SIZE GRBM_GUI_ACTIVE GRBM_COUNT || exit $?

@@ -274,7 +274,6 @@ static int compare_wave(uint64_t B) {
         (void)hipMalloc(&p, kSinkBytes);
         (void)hipMemset(p, 0, kSinkBytes);
         g_sink.rep = (unsigned long long*)p;
-        g_sink.ticket = (unsigned int*)((char*)p + kSinkReplicas * kSinkRepStride * 8);
     }
     uint64_t *d1, *d2, *c1, *c2;
     uint8_t *o1, *o2;
@@ -467,7 +466,7 @@ int main(int argc, char** argv) {
         void* sp = nullptr;
         (void)hipMalloc(&sp, kSinkBytes);
         (void)hipMemset(sp, 0, kSinkBytes);
-        Sink sk{(unsigned long long*)sp, (unsigned int*)((char*)sp + kSinkReplicas * kSinkRepStride * 8)};
+        Sink sk{(unsigned long long*)sp};
         const uint64_t words = (B + 63) / 64, tasks = (words + Om3W<10>::W - 1) / Om3W<10>::W;
         GenSpec gs{1, 3, 1, 1};
         const float us = time_launch(k_om3w<10>, (uint32_t)((tasks + 3) / 4), 4 * Om3W<10>::words * 8,

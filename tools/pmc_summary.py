@@ -18,9 +18,13 @@ from __future__ import annotations
 import collections
 import csv
 import glob
+import hashlib
 import json
 import os
 import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "byzantine-agreement_amd", "ba_amd", "libba_hip.so")
 
 SIMDS = 256 * 4
 
@@ -49,8 +53,10 @@ def main():
             e["kernel_cycles"] = cyc
             e["valu_util"] = mean["SQ_INSTS_VALU"] * 2 / (SIMDS * cyc)
         res[k] = e
-    json.dump({"source": d, "workload": workload, "config": config, "kernels": res},
-              open(out, "w"), indent=1)
+    # the build these counters belong to (bench.py matches it before quoting them)
+    sha = hashlib.sha256(open(LIB, "rb").read()).hexdigest()[:16] if os.path.exists(LIB) else None
+    json.dump({"source": d, "workload": workload, "config": config, "lib_sha16": sha,
+               "kernels": res}, open(out, "w"), indent=1)
     for k, e in res.items():
         print(k[:50], {x: e[x] for x in e if x not in ("counters",)})
 

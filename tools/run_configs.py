@@ -1,4 +1,6 @@
-"""BASELINE.json configs 3-5 (the non-headline ones) through ba_amd.dist.
+"""BASELINE.json configs 3-5 (the non-headline ones) through the C ABI's
+multi-GPU entries (ba_run_trials_multi, ba_run_instance_split_multi; ba_amd.dist
+does the rendezvous).
 
     python tools/run_configs.py [--only 3,4,5]                       # one GPU
     python -m torch.distributed.run --nproc-per-node N tools/run_configs.py  # N GPUs
@@ -10,7 +12,8 @@
      of 1024 instances (throughput), votes all-gathered across ranks
 
 Rank 0 prints one JSON line per config.  Timings bracket the device work with
-torch.cuda.synchronize() (+ a barrier across ranks) and take the max over ranks.
+torch.cuda.synchronize() (+ a gloo barrier across ranks) and take the max over
+ranks; the collectives themselves are RCCL inside libba_hip.
 """
 from __future__ import annotations
 
@@ -37,13 +40,15 @@ def timed(fn, world, dev):
     t0 = time.perf_counter()
     out = fn()
     torch.cuda.synchronize(dev)
-    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     return out, float(dt.item())
 
 
 def counters(t):
+    if isinstance(t, dict):
+        return t
     return dict(zip(L.COUNTER_NAMES, [int(x) for x in t.cpu().tolist()]))
 
 
@@ -58,26 +63,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # rehearsal knobs for a one-GPU box (as in bench.py): every rank on cuda:0,
-    # gloo in place of RCCL (which refuses two ranks on one device)
-    if os.environ.get("BA_BENCH_SHARE_GPU") == "1":
-        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        backend = os.environ.get("BA_BENCH_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group("gloo")  # rendezvous + barriers; RCCL runs inside the C ABI
     eng = L.Engine(local)
-    be = D.DeviceBackend(eng, dev)
+    comm = D.init_comm(eng)  # a one-rank communicator on one GPU
     out = []
 
     if 3 in which:
         n, m, T = 13, 4, a.trials3
-        D.run_trials_dp(be, n, m, 1 << 16, f=4)  # warm-up: geometry, scratch
-        cnt, dt = timed(lambda: D.run_trials_dp(be, n, m, T, f=4), world, dev)
+        D.run_trials_dp(comm, n, m, 1 << 16, f=4)  # warm-up: geometry, scratch
+        cnt, dt = timed(lambda: D.run_trials_dp(comm, n, m, T, f=4), world, dev)
         out.append({"config": 3, "workload": f"OM({m}) n={n}, {T} trials, f~U{{0..4}}, "
                     f"trial-DP over {world} GPU(s), counters all-reduced",
                     "trials_per_s": T / dt, "seconds": dt, "n_gpus": world,
@@ -85,10 +82,10 @@ def main():
 
     if 4 in which:
         n, m, T = 10, 3, a.trials4
-        D.run_trials_dp(be, n, m, 1 << 16, f=1)  # warm-up
+        D.run_trials_dp(comm, n, m, 1 << 16, f=1)  # warm-up
         rows = []
         for f in range(0, (n - 1) // 3 + 2):
-            cnt, dt = timed(lambda: D.run_trials_dp(be, n, m, T, f=f, faulty_mode=L.FAULTY_EXACT,
+            cnt, dt = timed(lambda: D.run_trials_dp(comm, n, m, T, f=f, faulty_mode=L.FAULTY_EXACT,
                                                     base_trial=T * f), world, dev)
             c = counters(cnt)
             rows.append({"f": f, "agreement": c["agreement"] / T,
@@ -107,19 +104,21 @@ def main():
         for B in (1, a.batch5):
             p = L.make_params(n, m, 0xBA5EED, L.LIE_PHILOX, L.FAULTY_RANDOM, 5, L.ORDER_RANDOM,
                               L.ATTACK, L.ENGINE_LEVELS, 0)
-            D.run_instance_split(be, p, B)  # warm-up
+            D.run_instance_split(comm, p, B, dev)  # warm-up
             reps = 10 if B == 1 else 3
-            (dec, o, cnt), dt = timed(lambda: [D.run_instance_split(be, p, B)
+            (dec, o, cnt), dt = timed(lambda: [D.run_instance_split(comm, p, B, dev)
                                                for _ in range(reps)][-1], world, dev)
             res[B] = {"seconds_per_call": dt / reps, "instances_per_s": B * reps / dt,
                       "counters": counters(cnt)}
-            # the same call replayed from hipGraphs (D.InstanceSplitGraphs)
-            g = D.InstanceSplitGraphs(eng, dev, p, B)
-            (gd, go, gc), gdt = timed(lambda: [g.replay() for _ in range(reps)][-1], world, dev)
-            if not (torch.equal(gd, dec) and torch.equal(go, o) and torch.equal(gc, cnt)):
+            # the same call replayed from hipGraphs (D.InstanceSplitGraphs, its own ctx)
+            g = D.InstanceSplitGraphs(dev, p, B, comm if world > 1 else None)
+            reps_g = 50 if B == 1 else 10
+            (gd, go, gc), gdt = timed(lambda: [g.replay() for _ in range(reps_g)][-1], world, dev)
+            if not (torch.equal(gd, dec) and torch.equal(go, o) and counters(gc) == counters(cnt)):
                 raise SystemExit("config 5: graph replay differs from the eager split")
-            res[B]["graph_seconds_per_call"] = gdt / reps
-            res[B]["graph_instances_per_s"] = B * reps / gdt
+            res[B]["graph_seconds_per_call"] = gdt / reps_g
+            res[B]["graph_instances_per_s"] = B * reps_g / gdt
+            g.close()
         out.append({"config": 5, "workload": f"OM({m}) n={n} (3,999,675 tree slots), first-hop "
                     f"subtree split over {world} GPU(s), votes all-gathered",
                     "latency_one_instance_ms": res[1]["seconds_per_call"] * 1e3,
@@ -131,6 +130,7 @@ def main():
     if rank == 0:
         for line in out:
             print(json.dumps(line), flush=True)
+    comm.close()
     if world > 1:
         dist.destroy_process_group()
     eng.close()
