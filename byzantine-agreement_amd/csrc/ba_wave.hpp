@@ -348,6 +348,110 @@ __device__ __forceinline__ void wave_alternate_priority(uint32_t round) {
 }
 
 // ---------------------------------------------------------------------------
+// One first-hop round j1 of the depth-3 WAVE kernels (k_om3w, k_om3q): lane
+// (lw, la) resolves leaf block (j1, la) of trial word lw, then R1[j1, b] for
+// b = la, which it returns (the receiver is lieutenant j2 = la + (la >= j1)).
+//   in     the word's input planes F[N] OB OO VAL (LDS)
+//   l0j1   L0[j1] of word lw
+//   r2t    the wave's R2T scratch [W][C][C+1] (LDS): receiver-major, rows
+//          padded to C+1 words so the column reads of step 3 are free of bank
+//          conflicts (stride 9 words = 18 banks for n=10: 32 distinct bank pairs)
+// Every lane of the wave calls it (it holds a wave barrier); lanes with !act
+// return 0.
+// ---------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ uint64_t om3_round(const uint64_t* in, uint64_t l0j1, uint64_t* r2t_w,
+                                              uint32_t lw, uint32_t la, bool act, uint32_t j1,
+                                              uint64_t seed, uint64_t gw) {
+    constexpr int L = N - 1, S = N - 3, C = L - 1, CP = C + 1;
+    constexpr uint32_t ME = 3;
+    const uint32_t sr = j1 * C + la;             // level-1 slot (j1, j2)
+    const uint32_t j2 = la + (la >= j1);
+    if (act) {
+        // 1. L1[j1, a] (sender j1 relays L0[j1]) and the level-2 diagonal
+        //    pairs of leaf block (j1, a): one interleaved Philox group
+        const uint32_t x0 = sr * S;
+        constexpr int NPD = (S + 1) / 2;
+        uint64_t lw2[2 * NPD], lie;
+        if constexpr (S % 2 == 1 && C % 2 == 0) {
+            // Lanes a, a^1 hold leaf blocks sr even / odd of one word: they
+            // share the level-1 pair sr>>1 and one level-2 pair (the even
+            // block's last = the odd block's first), 2*NPD distinct calls
+            // for the two.  Each lane issues NPD of them and takes the
+            // missing one from its partner: the even lane the shared
+            // level-2 pair, the odd lane the level-1 pair.
+            const bool odd = (sr & 1u) != 0;
+            const uint32_t d0 = x0 >> 1;  // first level-2 pair of this block
+            P4 pc[NPD];
+            static_for<0, NPD>([&](auto qd) {
+                const bool l1 = !odd && qd() == NPD - 1;
+                pc[qd()] = P4{l1 ? (sr >> 1) : d0 + qd(), l1 ? 1u : 2u, (uint32_t)gw,
+                              (uint32_t)(gw >> 32)};
+            });
+            philox10_n<NPD>(pc, (uint32_t)seed, (uint32_t)(seed >> 32));
+            // even lane sends its level-1 pair, odd lane its first level-2 pair
+            P4 snd = odd ? pc[0] : pc[NPD - 1], rcv;
+            rcv.x = __shfl_xor(snd.x, 1, 64);
+            rcv.y = __shfl_xor(snd.y, 1, 64);
+            rcv.z = __shfl_xor(snd.z, 1, 64);
+            rcv.w = __shfl_xor(snd.w, 1, 64);
+            const P4 p1 = odd ? rcv : pc[NPD - 1];
+            static_for<0, NPD>([&](auto qd) {
+                const P4 q = (qd() == NPD - 1 && !odd) ? rcv : pc[qd()];
+                lw2[2 * qd()] = (uint64_t)q.y << 32 | q.x;
+                lw2[2 * qd() + 1] = (uint64_t)q.w << 32 | q.z;
+            });
+            lie = odd ? ((uint64_t)p1.w << 32 | p1.z) : ((uint64_t)p1.y << 32 | p1.x);
+        } else {
+            P4 pc[NPD + 1];
+            static_for<0, NPD>([&](auto qd) {
+                pc[qd()] = P4{(x0 >> 1) + qd(), 2u, (uint32_t)gw, (uint32_t)(gw >> 32)};
+            });
+            pc[NPD] = P4{sr >> 1, 1u, (uint32_t)gw, (uint32_t)(gw >> 32)};
+            philox10_n<NPD + 1>(pc, (uint32_t)seed, (uint32_t)(seed >> 32));
+            static_for<0, NPD>([&](auto qd) {
+                lw2[2 * qd()] = (uint64_t)pc[qd()].y << 32 | pc[qd()].x;
+                lw2[2 * qd() + 1] = (uint64_t)pc[qd()].w << 32 | pc[qd()].z;
+            });
+            lie = (sr & 1u) ? ((uint64_t)pc[NPD].w << 32 | pc[NPD].z)
+                            : ((uint64_t)pc[NPD].y << 32 | pc[NPD].x);
+        }
+        const uint64_t fj = in[j1 + 1];
+        const uint64_t par = (fj & lie) | (~fj & l0j1);
+        // 2. leaf block (j1, a): level-2 diagonal, then S(S-1) leaves
+        const uint32_t lo = j1 < j2 ? j1 : j2, hi = j1 < j2 ? j2 : j1;
+        const uint64_t fs = in[j2 + 1];  // level-2 sender: j2
+        const uint64_t oddmask = 0ull - (uint64_t)(x0 & 1u);
+        uint64_t diag[S], Fm[S], R[S];
+        static_for<0, S>([&](auto a) {
+            uint64_t lie2;
+            if constexpr (S % 2 == 1) lie2 = lw2[a()] ^ ((lw2[a()] ^ lw2[a() + 1]) & oddmask);
+            else lie2 = lw2[a()];
+            diag[a()] = (fs & lie2) | (~fs & par);
+            const uint32_t ida = a() + (a() >= lo) + (a() + 1 >= hi);  // member a's rank
+            Fm[a()] = in[ida + 1];
+        });
+        leaf_block<S>(ME, seed, gw, sr, diag, Fm, R);
+        // receiver-major: member d of block a is receiver b = d + (d >= a)
+        uint64_t* r2t = r2t_w + lw * C * CP + la;
+        r2t[la * CP] = par;
+        static_for<0, S>([&](auto d) { r2t[(d() + (d() >= la ? 1u : 0u)) * CP] = R[d()]; });
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint64_t r1 = 0;
+    if (act) {
+        // 3. R1[j1, b], b = la: L1[j1, b] (this lane's own parent) plus
+        //    column b of the word's other leaf blocks a' != b
+        const uint64_t* col = r2t_w + (lw * C + la) * CP;
+        Csa<planes_c(C)> cnt;
+        static_for<0, C>([&](auto a) { cnt.template add<a()>(col[a()]); });
+        r1 = cnt.template ge<C, C / 2 + 1>();  // inner tie -> non-attack
+    }
+    __builtin_amdgcn_wave_barrier();  // r2t is rewritten by the next round
+    return r1;
+}
+
+// ---------------------------------------------------------------------------
 // k_om3w: effective depth 3 (see the WAVE engine note above)
 // ---------------------------------------------------------------------------
 template <int N>
@@ -357,9 +461,10 @@ struct Om3W {
     static constexpr int LANES = W * C;            // lanes busy in the subtree rounds
     static constexpr int P = planes_c(L);          // root counter planes (L inputs)
     static constexpr int NIN = N + 3;
-    static constexpr int oIN = 0, oL0 = oIN + W * NIN, oR2 = oL0 + W * L, oRC = oR2 + W * C * C;
+    static constexpr int CP = C + 1;               // padded R2T row (om3_round)
+    static constexpr int oIN = 0, oL0 = oIN + W * NIN, oR2 = oL0 + W * L, oRC = oR2 + W * C * CP;
     static constexpr int end0 = oRC + W * L * P;
-    static constexpr bool au_in_r2 = 2 * L <= C * C;
+    static constexpr bool au_in_r2 = 2 * L <= C * CP;
     static constexpr int oAU = au_in_r2 ? oR2 : end0;
     static constexpr int words = ((au_in_r2 ? end0 : end0 + W * 2 * L) + 1) & ~1;
 };
@@ -372,7 +477,7 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
     uint64_t* __restrict__ decisions, uint8_t* __restrict__ outcome,
     uint64_t* __restrict__ counters, Sink sk) {
     using G = Om3W<N>;
-    constexpr int L = G::L, S = G::S, C = G::C, W = G::W, P = G::P, NIN = G::NIN;
+    constexpr int L = G::L, C = G::C, W = G::W, P = G::P, NIN = G::NIN;
     constexpr uint32_t ME = 3;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
@@ -402,91 +507,11 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
         const uint64_t gw = gw0 + lw;
         for (uint32_t j1 = 0; j1 < (uint32_t)L; ++j1) {
             if constexpr ((DIAG & 8) == 0) wave_alternate_priority(j1);
-            const uint32_t sr = j1 * C + la;             // level-1 slot (j1, j2)
-            const uint32_t j2 = la + (la >= j1);
-            uint64_t par = 0;
-            if (act) {
-                // 1. L1[j1, a] (sender j1 relays L0[j1]) and the level-2 diagonal
-                //    pairs of leaf block (j1, a): one interleaved Philox group
-                const uint32_t x0 = sr * S;
-                constexpr int NPD = (S + 1) / 2;
-                uint64_t lw2[2 * NPD], lie;
-                if constexpr (S % 2 == 1 && C % 2 == 0) {
-                    // Lanes a, a^1 hold leaf blocks sr even / odd of one word: they
-                    // share the level-1 pair sr>>1 and one level-2 pair (the even
-                    // block's last = the odd block's first), 2*NPD distinct calls
-                    // for the two.  Each lane issues NPD of them and takes the
-                    // missing one from its partner: the even lane the shared
-                    // level-2 pair, the odd lane the level-1 pair.
-                    const bool odd = (sr & 1u) != 0;
-                    const uint32_t d0 = x0 >> 1;  // first level-2 pair of this block
-                    P4 pc[NPD];
-                    static_for<0, NPD>([&](auto qd) {
-                        const bool l1 = !odd && qd() == NPD - 1;
-                        pc[qd()] = P4{l1 ? (sr >> 1) : d0 + qd(), l1 ? 1u : 2u, (uint32_t)gw,
-                                      (uint32_t)(gw >> 32)};
-                    });
-                    philox10_n<NPD>(pc, (uint32_t)seed, (uint32_t)(seed >> 32));
-                    // even lane sends its level-1 pair, odd lane its first level-2 pair
-                    P4 snd = odd ? pc[0] : pc[NPD - 1], rcv;
-                    rcv.x = __shfl_xor(snd.x, 1, 64);
-                    rcv.y = __shfl_xor(snd.y, 1, 64);
-                    rcv.z = __shfl_xor(snd.z, 1, 64);
-                    rcv.w = __shfl_xor(snd.w, 1, 64);
-                    const P4 p1 = odd ? rcv : pc[NPD - 1];
-                    static_for<0, NPD>([&](auto qd) {
-                        const P4 q = (qd() == NPD - 1 && !odd) ? rcv : pc[qd()];
-                        lw2[2 * qd()] = (uint64_t)q.y << 32 | q.x;
-                        lw2[2 * qd() + 1] = (uint64_t)q.w << 32 | q.z;
-                    });
-                    lie = odd ? ((uint64_t)p1.w << 32 | p1.z) : ((uint64_t)p1.y << 32 | p1.x);
-                } else {
-                    P4 pc[NPD + 1];
-                    static_for<0, NPD>([&](auto qd) {
-                        pc[qd()] = P4{(x0 >> 1) + qd(), 2u, (uint32_t)gw, (uint32_t)(gw >> 32)};
-                    });
-                    pc[NPD] = P4{sr >> 1, 1u, (uint32_t)gw, (uint32_t)(gw >> 32)};
-                    philox10_n<NPD + 1>(pc, (uint32_t)seed, (uint32_t)(seed >> 32));
-                    static_for<0, NPD>([&](auto qd) {
-                        lw2[2 * qd()] = (uint64_t)pc[qd()].y << 32 | pc[qd()].x;
-                        lw2[2 * qd() + 1] = (uint64_t)pc[qd()].w << 32 | pc[qd()].z;
-                    });
-                    lie = (sr & 1u) ? ((uint64_t)pc[NPD].w << 32 | pc[NPD].z)
-                                    : ((uint64_t)pc[NPD].y << 32 | pc[NPD].x);
-                }
-                const uint64_t fj = in[j1 + 1];
-                par = (fj & lie) | (~fj & img[G::oL0 + lw * L + j1]);
-                // 2. leaf block (j1, a): level-2 diagonal, then S(S-1) leaves
-                const uint32_t lo = j1 < j2 ? j1 : j2, hi = j1 < j2 ? j2 : j1;
-                const uint64_t fs = in[j2 + 1];  // level-2 sender: j2
-                const uint64_t oddmask = 0ull - (uint64_t)(x0 & 1u);
-                uint64_t diag[S], Fm[S], R[S];
-                static_for<0, S>([&](auto a) {
-                    uint64_t lie2;
-                    if constexpr (S % 2 == 1) lie2 = lw2[a()] ^ ((lw2[a()] ^ lw2[a() + 1]) & oddmask);
-                    else lie2 = lw2[a()];
-                    diag[a()] = (fs & lie2) | (~fs & par);
-                    const uint32_t ida = a() + (a() >= lo) + (a() + 1 >= hi);  // member a's rank
-                    Fm[a()] = in[ida + 1];
-                });
-                leaf_block<S>(ME, seed, gw, sr, diag, Fm, R);
-                // receiver-major: member d of block a is receiver b = d + (d >= a)
-                uint64_t* r2t = img + G::oR2 + lw * C * C + la;
-                r2t[la * C] = par;
-                static_for<0, S>([&](auto d) { r2t[(d() + (d() >= la ? 1u : 0u)) * C] = R[d()]; });
-            }
-            __builtin_amdgcn_wave_barrier();
+            const uint64_t r1 = om3_round<N>(in, act ? img[G::oL0 + lw * L + j1] : 0ull,
+                                             img + G::oR2, lw, la, act, j1, seed, gw);
             FUSED_STAMP(1);
-            if (act) {
-                // 3. R1[j1, b], b = la: L1[j1, b] (this lane's own parent) plus
-                //    column b of the word's other leaf blocks a' != b
-                const uint64_t* col = img + G::oR2 + (lw * C + la) * C;
-                Csa<planes_c(C)> cnt;
-                static_for<0, C>([&](auto a) { cnt.template add<a()>(col[a()]); });
-                const uint64_t r1 = cnt.template ge<C, C / 2 + 1>();  // inner tie -> non-attack
-                // root column j2 += R1[j1, b] (ripple add on the bit-sliced planes)
-                planes_add<P>(img + G::oRC + (lw * L + j2) * P, r1);
-            }
+            // root column j2 += R1[j1, b] (ripple add on the bit-sliced planes)
+            if (act) planes_add<P>(img + G::oRC + (lw * L + la + (la >= j1 ? 1u : 0u)) * P, r1);
             __builtin_amdgcn_wave_barrier();
             FUSED_STAMP(2);
         }
@@ -511,6 +536,204 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
         g_fused_stamps[blockIdx.x * wpb + wv][7] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// k_om3q: effective depth 3 with a block-level work queue (the bench kernel).
+//
+// k_om3w gives each wave a whole task (W words x all L first-hop rounds).  At
+// two waves per SIMD the SIMD's older wave wins VALU arbitration, finishes its
+// task first and leaves the younger wave alone for the last ~25% of the
+// launch at about half the issue rate (tools/om3_lab HW_ID trace, round 2).
+// k_om3q cuts the work finer: a block of 8 waves (two per SIMD) holds up to
+// kQueueMaxTasks tasks in LDS, and a UNIT is one first-hop round j1 of one
+// task (one om3_round: 1/L of the task).  Waves take units from an LDS
+// counter, so a faster wave simply takes more of them; the wave that finishes
+// the L-th unit of a task resolves that task's roots and epilogue while the
+// others keep taking units.  Phases per group of tasks:
+//   A. inputs + level 0 of each task (one wave per task), L0 also written on
+//      the diagonal of the task's R1T
+//   B. units (task-major, so tasks complete one after another): om3_round,
+//      then R1[j1, b] stored receiver-major, R1T[w][j2][j1]; no counters are
+//      accumulated per round (k_om3w's LDS read-modify-write of root planes)
+//   C. (by the L-th unit's wave) roots = compile-time carry-save counts of the
+//      L contiguous R1T words, then the shared epilogue
+// Bit-identical to k_om3w (same lie keying, same majorities).
+// LDS: per task IN[W][N+3] | L0[W][L] | R1T[W][L][L]; per wave the R2T
+// scratch [W][C][C+1] (the roots' A/U reuse it).
+// ---------------------------------------------------------------------------
+constexpr int kQueueThreads = 512;  // 8 waves: two per SIMD
+constexpr int kQueueMaxTasks = 8;   // tasks a block holds in LDS at once
+
+template <int N>
+struct Om3Q {
+    static constexpr int L = N - 1, S = N - 3, C = L - 1, CP = C + 1;
+    static constexpr int W = 64 / C;
+    static constexpr int LANES = W * C;
+    static constexpr int NIN = N + 3;
+    static constexpr int tIN = 0, tL0 = W * NIN, tR1 = tL0 + W * L;
+    static constexpr int task_words = ((tR1 + W * L * L) + 1) & ~1;
+    static constexpr int wave_words = ((W * C * CP > W * 2 * L ? W * C * CP : W * 2 * L) + 1) & ~1;
+    static constexpr int waves = kQueueThreads / 64;
+    static constexpr int lds_bytes = (kQueueMaxTasks * task_words + waves * wave_words) * 8;
+};
+
+// Level 0 of a task's W words (one Philox per slot pair) into l0[w*L + j] and
+// the diagonal r1t[(w*L + j)*L + j] (root column j counts L0[j] as its own input).
+template <int N, int W>
+__device__ __forceinline__ void queue_level0(const uint64_t* in0, uint64_t* l0, uint64_t* r1t,
+                                             uint32_t lane, uint64_t seed, uint64_t gw0) {
+    constexpr int L = N - 1, NIN = N + 3;
+    constexpr uint32_t NP0 = (L + 1) / 2;
+    for (uint32_t it = lane; it < (uint32_t)W * NP0; it += 64) {
+        const uint32_t w = it / NP0, p = it - w * NP0;
+        const uint64_t* in = in0 + w * NIN;
+        const uint64_t F0 = in[0], ob = in[N];
+        uint64_t lv[2];
+        lie_pair(seed, 0, p, gw0 + w, lv[0], lv[1]);
+        static_for<0, 2>([&](auto h) {
+            const uint32_t j = 2 * p + h();
+            if (j < (uint32_t)L) {
+                const uint64_t v = (F0 & lv[h()]) | (~F0 & ob);
+                l0[w * L + j] = v;
+                r1t[(w * L + j) * L + j] = v;
+            }
+        });
+    }
+}
+
+// Run counters of a block of WAVES waves: wave sums (lane c holds counter c),
+// combined in LDS, then one sink unit per block (contains a block barrier).
+template <int WAVES>
+__device__ __forceinline__ void block_flush(const TrialCounts& tc, uint32_t lane, uint32_t wv,
+                                            uint64_t* __restrict__ counters, const Sink& sk) {
+    uint64_t mine = 0;
+#pragma unroll
+    for (int c = 0; c < C_NUM; ++c) {
+        uint32_t x = tc.v[c];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+        if (lane == (uint32_t)c) mine = x;
+    }
+    __shared__ unsigned long long wcnt[WAVES][16];
+    if (lane < 16) wcnt[wv][lane] = mine;
+    __syncthreads();
+    if (wv == 0) {
+        uint64_t tot = 0;
+        for (uint32_t k = 0; k < (uint32_t)WAVES; ++k) tot += lane < 16 ? wcnt[k][lane] : 0;
+        sink_counters(lane, tot, blockIdx.x, gridDim.x, counters, sk);
+    }
+}
+
+// STAGED: both inputs given (ba_gen_inputs_device buffers): loads only, the
+// draw code is not compiled in.
+template <int N, bool STAGED>
+__global__ __launch_bounds__(kQueueThreads, 2) void k_om3q(
+    uint64_t seed, GenSpec gs, uint64_t first_trial, uint64_t batch,
+    const uint32_t* __restrict__ faulty, const uint8_t* __restrict__ order,
+    uint64_t* __restrict__ decisions, uint8_t* __restrict__ outcome,
+    uint64_t* __restrict__ counters, Sink sk, uint32_t tasks_per_group) {
+    using G = Om3Q<N>;
+    constexpr int L = G::L, C = G::C, W = G::W, NIN = G::NIN, WAVES = G::waves;
+    constexpr uint32_t ME = 3;
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    __shared__ uint32_t q_next, q_done[kQueueMaxTasks];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t* wimg = lds + kQueueMaxTasks * G::task_words + wv * G::wave_words;
+    const uint64_t total_words = (batch + 63) / 64;
+    const uint64_t ntasks = (total_words + W - 1) / W;
+    const uint64_t ngroups = (ntasks + tasks_per_group - 1) / tasks_per_group;
+    const uint32_t lw_ = lane / C, la = lane - lw_ * C;
+    const bool act = lane < (uint32_t)G::LANES;
+    const uint32_t lw = act ? lw_ : 0;
+    TrialCounts tc;
+    for (uint64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+        const uint64_t t0 = grp * tasks_per_group;
+        const uint32_t nt = (uint32_t)(ntasks - t0 < tasks_per_group ? ntasks - t0 : tasks_per_group);
+        if (threadIdx.x == 0) q_next = 0;
+        if (threadIdx.x < (uint32_t)kQueueMaxTasks) q_done[threadIdx.x] = 0;
+        // A. inputs + level 0, one wave per task
+        for (uint32_t t = wv; t < nt; t += WAVES) {
+            uint64_t* timg = lds + t * G::task_words;
+            const uint64_t w0 = (t0 + t) * W;
+            if constexpr (STAGED)
+                gen_words<N, W, -1>(timg + G::tIN, lane, w0, seed, gs, first_trial, batch, faulty, order);
+            else
+                wave_inputs<N, W, 0>(timg + G::tIN, lane, w0, seed, gs, first_trial, batch, faulty, order);
+            __builtin_amdgcn_wave_barrier();
+            queue_level0<N, W>(timg + G::tIN, timg + G::tL0, timg + G::tR1, lane, seed,
+                               (first_trial >> 6) + w0);
+        }
+        __syncthreads();
+        // B. units (task, j1), task-major, from the block's queue
+        const uint32_t nunits = nt * (uint32_t)L;
+        while (true) {
+            uint32_t u = 0;
+            if (lane == 0) u = atomicAdd(&q_next, 1u);
+            u = __builtin_amdgcn_readfirstlane(u);
+            if (u >= nunits) break;
+            const uint32_t t = u / (uint32_t)L, j1 = u - t * (uint32_t)L;
+            uint64_t* timg = lds + t * G::task_words;
+            const uint64_t w0 = (t0 + t) * W;
+            const uint64_t gw = (first_trial >> 6) + w0 + lw;
+            const uint64_t r1 = om3_round<N>(timg + G::tIN + lw * NIN,
+                                             act ? timg[G::tL0 + lw * L + j1] : 0ull, wimg, lw, la,
+                                             act, j1, seed, gw);
+            if (act) timg[G::tR1 + (lw * L + la + (la >= j1 ? 1u : 0u)) * L + j1] = r1;
+            // the L-th finished unit of a task resolves it: its R1T writes (and every
+            // other wave's) are ordered before the counter by the workgroup release
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            uint32_t d = 0;
+            if (lane == 0) d = atomicAdd(&q_done[t], 1u);
+            d = __builtin_amdgcn_readfirstlane(d);
+            if (d + 1 != (uint32_t)L) continue;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            // C. roots: column j2 of word w = L contiguous words (L0 on the diagonal)
+            for (uint32_t it = lane; it < (uint32_t)(W * L); it += 64) {
+                const uint32_t w = it / L, col = it - w * L;
+                const uint64_t* r1t = timg + G::tR1 + (w * L + col) * L;
+                Csa<planes_c(L)> cnt;
+                static_for<0, L>([&](auto j) { cnt.template add<j()>(r1t[j()]); });
+                const uint64_t att = cnt.template ge<L, L / 2 + 1>();
+                uint64_t tie = 0;
+                if constexpr (L % 2 == 0) tie = cnt.template ge<L, L / 2>() & ~att;  // root tie: undefined
+                wimg[w * 2 * L + col] = att;
+                wimg[w * 2 * L + L + col] = tie;
+            }
+            __builtin_amdgcn_wave_barrier();
+            wave_epilogue<N, W, ME, 0>(timg + G::tIN, wimg, lane, w0, batch, decisions, outcome, tc);
+            __builtin_amdgcn_wave_barrier();
+        }
+        __syncthreads();
+    }
+    block_flush<WAVES>(tc, lane, wv, counters, sk);
+}
+
+template <int N>
+inline hipError_t launch_om3q(const RunArgs& a) {
+    using G = Om3Q<N>;
+    const uint64_t words = (a.batch + 63) / 64, tasks = (words + G::W - 1) / G::W;
+    // enough groups for every CU, at most kQueueMaxTasks tasks per group
+    uint64_t tpg = (tasks + a.cu_count - 1) / a.cu_count;
+    if (tpg < 1) tpg = 1;
+    if (tpg > (uint64_t)kQueueMaxTasks) tpg = kQueueMaxTasks;
+    const uint64_t groups = (tasks + tpg - 1) / tpg;
+    uint64_t blocks = groups < a.cu_count ? groups : a.cu_count;  // one 8-wave block per CU
+    if (const char* e = getenv("BA_WAVE_MAX_BLOCKS")) {  // tests: force the persistent group loop
+        const uint64_t c = strtoull(e, nullptr, 0);
+        if (c >= 1 && c < blocks) blocks = c;
+    }
+    const bool staged = a.gen.faulty_mode == 0 && a.gen.order_mode == 0;
+    ProfScope ps(a.prof, "k_om3q", a.stream);
+    if (staged)
+        hipLaunchKernelGGL((k_om3q<N, true>), dim3((uint32_t)blocks), dim3(kQueueThreads),
+                           G::lds_bytes, a.stream, a.seed, a.gen, a.first_trial, a.batch, a.faulty,
+                           a.order, a.decisions, a.outcome, a.counters, a.sink, (uint32_t)tpg);
+    else
+        hipLaunchKernelGGL((k_om3q<N, false>), dim3((uint32_t)blocks), dim3(kQueueThreads),
+                           G::lds_bytes, a.stream, a.seed, a.gen, a.first_trial, a.batch, a.faulty,
+                           a.order, a.decisions, a.outcome, a.counters, a.sink, (uint32_t)tpg);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

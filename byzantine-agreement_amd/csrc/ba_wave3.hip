@@ -14,6 +14,18 @@ bool wave_supported(const Geometry& g) {
 hipError_t launch_wave_engine(const RunArgs& a, const Geometry& g) {
     if (g.me == 4) return launch_wave4(a, g);
     if (g.me != 3) return hipErrorInvalidValue;
+    // depth 3: the queue kernel k_om3q; BA_WAVE_KIND=1 selects k_om3w (A/B, cross-checks)
+    const char* kind = getenv("BA_WAVE_KIND");
+    if (!(kind && kind[0] == '1')) {
+        switch (g.n) {
+#define OM3Q_CASE(nn) \
+    case nn: return launch_om3q<nn>(a);
+            OM3Q_CASE(5) OM3Q_CASE(6) OM3Q_CASE(7) OM3Q_CASE(8) OM3Q_CASE(9) OM3Q_CASE(10)
+            OM3Q_CASE(11) OM3Q_CASE(12) OM3Q_CASE(13) OM3Q_CASE(14)
+#undef OM3Q_CASE
+            default: return hipErrorInvalidValue;
+        }
+    }
     switch (g.n) {
 #define OM3W_CASE(nn) \
     case nn: return launch_wave<Om3W<nn>>(a, k_om3w<nn>, "k_om3w");

@@ -285,11 +285,11 @@ OM3_CASES = [(5, 3, 1, 1), (5, 4, 2, 1), (6, 3, 1, 2), (7, 3, 2, 1), (8, 3, 3, 1
 
 @pytest.mark.parametrize("n,m,f,fmode", OM3_CASES)
 def test_om3_wave_block_generic_vs_oracle(monkeypatch, n, m, f, fmode):
-    """k_om3w (default), k_fused3 (BA_FUSED_KIND=1) and k_fused (=2) against the
-    oracle, over every synthetic-input path of the WAVE kernel's branch-free
-    generator (f <= 2, 3, <= 6 and the generic fallback; random / exact /
-    given faulty sets), a ragged batch, and the persistent task loop
-    (BA_WAVE_MAX_BLOCKS=1: four waves walk all tasks)."""
+    """k_om3q (default), k_om3w (BA_WAVE_KIND=1), k_fused3 (BA_FUSED_KIND=1) and
+    k_fused (=2) against the oracle, over every synthetic-input path of the WAVE
+    kernels' branch-free generator (f <= 2, 3, <= 6 and the generic fallback;
+    random / exact / given faulty sets), a ragged batch, and the persistent
+    loops (BA_WAVE_MAX_BLOCKS=1: one block walks every task group)."""
     from ba_amd import lib as L
     B = 64 * 8 * 5 + 37
     if fmode == 0:
@@ -304,8 +304,10 @@ def test_om3_wave_block_generic_vs_oracle(monkeypatch, n, m, f, fmode):
                   L.ORDER_CONST, order_value=1, first_trial=64 * 77)
         ref = oracle_c.run(n, m, B, **kw)
     od, oo, ocnt = ref
-    for kind, cap in (("0", None), ("0", "1"), ("1", None), ("2", None)):
+    for kind, cap, wk in (("0", None, "0"), ("0", "1", "0"), ("0", None, "1"), ("0", "1", "1"),
+                          ("1", None, "0"), ("2", None, "0")):
         monkeypatch.setenv("BA_FUSED_KIND", kind)
+        monkeypatch.setenv("BA_WAVE_KIND", wk)
         if cap:
             monkeypatch.setenv("BA_WAVE_MAX_BLOCKS", cap)
         else:
@@ -315,10 +317,40 @@ def test_om3_wave_block_generic_vs_oracle(monkeypatch, n, m, f, fmode):
             res = e.run(n, m, B, engine=L.ENGINE_FUSED, **kw)
         finally:
             e.close()
-        tag = f"kind={kind} cap={cap} n={n} m={m} f={f} fmode={fmode}"
+        tag = f"kind={kind} wave={wk} cap={cap} n={n} m={m} f={f} fmode={fmode}"
         same(res.decisions, od, "decisions " + tag)
         same(res.outcome, oo, "outcome " + tag)
         assert {k: res.counters[k] for k in ocnt} == ocnt, tag
+
+
+@pytest.mark.parametrize("n,B", [(10, 64 * 8 * 700 + 5), (13, 64 * 5 * 600 + 63), (7, 64 * 16 * 300)])
+def test_om3q_task_groups_vs_oracle(engine, n, B):
+    """k_om3q with several tasks per block group (tpg = ceil(tasks / CUs) = 2..3) and a
+    ragged last group, staged and drawn inputs, against the oracle."""
+    import torch
+    from ba_amd import lib as L
+    kw = dict(seed=0xC0FFEE + n, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1,
+              order_mode=L.ORDER_RANDOM, first_trial=64 * 11)
+    od, oo, ocnt = oracle_c.run(n, 3, B, **kw)
+    res = engine.run(n, 3, B, **kw)
+    same(res.decisions, od, "drawn inputs")
+    same(res.outcome, oo, "drawn inputs")
+    assert {k: res.counters[k] for k in ocnt} == ocnt
+    fb = torch.empty(B, dtype=torch.int32, device="cuda")
+    ob = torch.empty(B, dtype=torch.uint8, device="cuda")
+    dec = torch.empty(B, dtype=torch.int64, device="cuda")
+    out = torch.empty(B, dtype=torch.uint8, device="cuda")
+    cnt = torch.zeros(16, dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    engine.gen_inputs_device(L.make_params(n, 3, **kw), B, d_faulty=fb.data_ptr(), d_order=ob.data_ptr(),
+                             stream=s)
+    p = L.make_params(n, 3, seed=kw["seed"], first_trial=kw["first_trial"])
+    engine.run_device(p, B, d_faulty=fb.data_ptr(), d_order=ob.data_ptr(), d_decisions=dec.data_ptr(),
+                      d_outcome=out.data_ptr(), d_counters=cnt.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    same(dec.cpu().numpy().view(np.uint64), od, "staged inputs")
+    same(out.cpu().numpy(), oo, "staged inputs")
+    assert cnt.cpu().tolist()[:12] == list(ocnt.values())
 
 
 @pytest.mark.parametrize("n,m,fmode,f,omode", [(10, 3, 1, 3, 1), (10, 3, 2, 4, 2), (13, 4, 1, 4, 1),
