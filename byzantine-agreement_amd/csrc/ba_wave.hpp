@@ -625,6 +625,45 @@ __device__ __forceinline__ void block_flush(const TrialCounts& tc, uint32_t lane
     }
 }
 
+// One trial word's epilogue with lane = trial (ba.py:197-255 via trial_result,
+// the restatement the oracle tests pin): the task's bit-sliced root words
+// A/U and input planes are read once each with wave-uniform (broadcast) LDS
+// reads, each lane gathers its own bits into lieutenant / general masks, and
+// stores its decision word and outcome byte.  A whole wave per word keeps the
+// epilogue parallel across waves (k_om3q queues it per word).
+template <int N, uint32_t ME>
+__device__ __forceinline__ void word_epilogue(const uint64_t* inw, const uint64_t* au,
+                                              uint32_t lane, uint64_t i, uint64_t batch,
+                                              uint64_t* __restrict__ decisions,
+                                              uint8_t* __restrict__ outcome, TrialCounts& tc) {
+    constexpr int L = N - 1;
+    const bool hi = lane >= 32;
+    const uint32_t sh = lane & 31;
+    auto bit = [&](uint64_t v) -> uint32_t {
+        return __builtin_amdgcn_ubfe(hi ? (uint32_t)(v >> 32) : (uint32_t)v, sh, 1);
+    };
+    uint64_t av[L], fv[N + 3];
+    static_for<0, L>([&](auto b) { av[b()] = au[b()]; });
+    static_for<0, N + 3>([&](auto g) { fv[g()] = inw[g()]; });
+    uint32_t A = 0, U = 0, fm = 0;
+    static_for<0, L>([&](auto b) { A |= bit(av[b()]) << (b() + 1); });
+    if constexpr (L % 2 == 0) {  // an even number of root inputs can tie: undefined
+        uint64_t uv[L];
+        static_for<0, L>([&](auto b) { uv[b()] = au[L + b()]; });
+        static_for<0, L>([&](auto b) { U |= bit(uv[b()]) << (b() + 1); });
+    }
+    static_for<0, N>([&](auto g) { fm |= bit(fv[g()]) << g(); });
+    const uint32_t live = bit(fv[N + 2]);
+    const uint32_t oc = bit(fv[N + 1]) ? 2u : bit(fv[N]);
+    if (live) {
+        uint64_t dec;
+        uint32_t out;
+        finish_trial(N, ME, fm, oc, A, U, dec, out, tc);
+        if (decisions) decisions[i] = dec;
+        if (outcome) outcome[i] = (uint8_t)out;
+    }
+}
+
 // STAGED: both inputs given (ba_gen_inputs_device buffers): loads only, the
 // draw code is not compiled in.
 template <int N, bool STAGED>
@@ -636,8 +675,13 @@ __global__ __launch_bounds__(kQueueThreads, 2) void k_om3q(
     using G = Om3Q<N>;
     constexpr int L = G::L, C = G::C, W = G::W, NIN = G::NIN, WAVES = G::waves;
     constexpr uint32_t ME = 3;
+    static_assert(G::W * G::L <= 128, "roots: two items per lane");
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-    __shared__ uint32_t q_next, q_done[kQueueMaxTasks];
+    // queue state: round units (q_next), per-task round completions (q_done);
+    // a task's W epilogue word units become available when its roots are
+    // written (e_ready) and are claimed one at a time (e_taken, e_claimed)
+    __shared__ uint32_t q_next, q_done[kQueueMaxTasks], e_ready[kQueueMaxTasks],
+        e_taken[kQueueMaxTasks], e_claimed;
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint64_t* wimg = lds + kQueueMaxTasks * G::task_words + wv * G::wave_words;
     const uint64_t total_words = (batch + 63) / 64;
@@ -650,8 +694,15 @@ __global__ __launch_bounds__(kQueueThreads, 2) void k_om3q(
     for (uint64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
         const uint64_t t0 = grp * tasks_per_group;
         const uint32_t nt = (uint32_t)(ntasks - t0 < tasks_per_group ? ntasks - t0 : tasks_per_group);
-        if (threadIdx.x == 0) q_next = 0;
-        if (threadIdx.x < (uint32_t)kQueueMaxTasks) q_done[threadIdx.x] = 0;
+        if (threadIdx.x == 0) {
+            q_next = 0;
+            e_claimed = 0;
+        }
+        if (threadIdx.x < (uint32_t)kQueueMaxTasks) {
+            q_done[threadIdx.x] = 0;
+            e_ready[threadIdx.x] = 0;
+            e_taken[threadIdx.x] = 0;
+        }
         // A. inputs + level 0, one wave per task
         for (uint32_t t = wv; t < nt; t += WAVES) {
             uint64_t* timg = lds + t * G::task_words;
@@ -665,44 +716,86 @@ __global__ __launch_bounds__(kQueueThreads, 2) void k_om3q(
                                (first_trial >> 6) + w0);
         }
         __syncthreads();
-        // B. units (task, j1), task-major, from the block's queue
-        const uint32_t nunits = nt * (uint32_t)L;
+        const uint32_t nunits = nt * (uint32_t)L, nepi = nt * (uint32_t)W;
         while (true) {
+            // 1. an epilogue word unit of a task whose roots are written, if any
+            uint32_t e = 0xFFFFFFFFu;
+            if (lane == 0) {
+                for (uint32_t t = 0; t < nt; ++t) {
+                    if (__hip_atomic_load(&e_ready[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &&
+                        __hip_atomic_load(&e_taken[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
+                            (uint32_t)W) {
+                        const uint32_t w = atomicAdd(&e_taken[t], 1u);
+                        if (w < (uint32_t)W) {
+                            atomicAdd(&e_claimed, 1u);
+                            e = t * W + w;
+                            break;
+                        }
+                    }
+                }
+            }
+            e = __builtin_amdgcn_readfirstlane(e);
+            if (e != 0xFFFFFFFFu) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                const uint32_t t = e / W, w = e - t * W;
+                const uint64_t* timg = lds + t * G::task_words;
+                const uint64_t wg = (t0 + t) * W + w;  // trial word within the batch
+                if (wg < total_words)
+                    word_epilogue<N, ME>(timg + G::tIN + w * NIN, timg + G::tR1 + w * 2 * L, lane,
+                                         wg * 64 + lane, batch, decisions, outcome, tc);
+                continue;
+            }
+            // 2. a round unit (task, j1), task-major
             uint32_t u = 0;
             if (lane == 0) u = atomicAdd(&q_next, 1u);
             u = __builtin_amdgcn_readfirstlane(u);
-            if (u >= nunits) break;
-            const uint32_t t = u / (uint32_t)L, j1 = u - t * (uint32_t)L;
-            uint64_t* timg = lds + t * G::task_words;
-            const uint64_t w0 = (t0 + t) * W;
-            const uint64_t gw = (first_trial >> 6) + w0 + lw;
-            const uint64_t r1 = om3_round<N>(timg + G::tIN + lw * NIN,
-                                             act ? timg[G::tL0 + lw * L + j1] : 0ull, wimg, lw, la,
-                                             act, j1, seed, gw);
-            if (act) timg[G::tR1 + (lw * L + la + (la >= j1 ? 1u : 0u)) * L + j1] = r1;
-            // the L-th finished unit of a task resolves it: its R1T writes (and every
-            // other wave's) are ordered before the counter by the workgroup release
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            uint32_t d = 0;
-            if (lane == 0) d = atomicAdd(&q_done[t], 1u);
-            d = __builtin_amdgcn_readfirstlane(d);
-            if (d + 1 != (uint32_t)L) continue;
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            // C. roots: column j2 of word w = L contiguous words (L0 on the diagonal)
-            for (uint32_t it = lane; it < (uint32_t)(W * L); it += 64) {
-                const uint32_t w = it / L, col = it - w * L;
-                const uint64_t* r1t = timg + G::tR1 + (w * L + col) * L;
-                Csa<planes_c(L)> cnt;
-                static_for<0, L>([&](auto j) { cnt.template add<j()>(r1t[j()]); });
-                const uint64_t att = cnt.template ge<L, L / 2 + 1>();
-                uint64_t tie = 0;
-                if constexpr (L % 2 == 0) tie = cnt.template ge<L, L / 2>() & ~att;  // root tie: undefined
-                wimg[w * 2 * L + col] = att;
-                wimg[w * 2 * L + L + col] = tie;
+            if (u < nunits) {
+                const uint32_t t = u / (uint32_t)L, j1 = u - t * (uint32_t)L;
+                uint64_t* timg = lds + t * G::task_words;
+                const uint64_t gw = (first_trial >> 6) + (t0 + t) * W + lw;
+                const uint64_t r1 = om3_round<N>(timg + G::tIN + lw * NIN,
+                                                 act ? timg[G::tL0 + lw * L + j1] : 0ull, wimg, lw,
+                                                 la, act, j1, seed, gw);
+                if (act) timg[G::tR1 + (lw * L + la + (la >= j1 ? 1u : 0u)) * L + j1] = r1;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                uint32_t d = 0;
+                if (lane == 0) d = atomicAdd(&q_done[t], 1u);
+                d = __builtin_amdgcn_readfirstlane(d);
+                if (d + 1 != (uint32_t)L) continue;
+                // the task's L-th round: its roots (compile-time carry-save counts of
+                // L contiguous R1T words, L0 on the diagonal; strict majority
+                // attacks, a tie is undefined, ba.py:188-195), written over R1T as
+                // AU[W][2L], then its W epilogue word units are queued
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                uint64_t att[2] = {0, 0}, tie[2] = {0, 0};
+                static_for<0, 2>([&](auto k) {
+                    const uint32_t it = lane + 64 * k();
+                    if (it < (uint32_t)(W * L)) {
+                        const uint32_t w = it / L, col = it - w * L;
+                        const uint64_t* r1t = timg + G::tR1 + (w * L + col) * L;
+                        Csa<planes_c(L)> cnt;
+                        static_for<0, L>([&](auto j) { cnt.template add<j()>(r1t[j()]); });
+                        att[k()] = cnt.template ge<L, L / 2 + 1>();
+                        if constexpr (L % 2 == 0) tie[k()] = cnt.template ge<L, L / 2>() & ~att[k()];
+                    }
+                });
+                __builtin_amdgcn_wave_barrier();
+                static_for<0, 2>([&](auto k) {
+                    const uint32_t it = lane + 64 * k();
+                    if (it < (uint32_t)(W * L)) {
+                        const uint32_t w = it / L, col = it - w * L;
+                        timg[G::tR1 + w * 2 * L + col] = att[k()];
+                        timg[G::tR1 + w * 2 * L + L + col] = tie[k()];
+                    }
+                });
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) __hip_atomic_store(&e_ready[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                continue;
             }
-            __builtin_amdgcn_wave_barrier();
-            wave_epilogue<N, W, ME, 0>(timg + G::tIN, wimg, lane, w0, batch, decisions, outcome, tc);
-            __builtin_amdgcn_wave_barrier();
+            // 3. nothing to take: done once every epilogue unit is claimed, else a
+            //    task's rounds are still running and its word units will appear
+            if (__hip_atomic_load(&e_claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= nepi) break;
+            __builtin_amdgcn_s_sleep(2);
         }
         __syncthreads();
     }
