@@ -224,6 +224,8 @@ template <int N, uint32_t ME>
 __device__ __forceinline__ void epilogue_planes(uint64_t* inw, const uint64_t* au,
                                                 TrialCounts& tc) {
     constexpr int L = N - 1, NB = planes_c(N);
+    // an odd number of root inputs never ties: no undefined decisions, U == 0
+    constexpr bool TIES = L % 2 == 0;
     constexpr int needed = N == 1 ? 1 : (N <= 3 ? N - 1 : 2 * ((N - 1) / 3) + 1);
     constexpr int K0 = L - needed;  // retreat: #(A|U) <= K0 (+1 when the commander retreats)
     const uint64_t val = inw[N + 2], oo = inw[N + 1];
@@ -232,25 +234,34 @@ __device__ __forceinline__ void epilogue_planes(uint64_t* inw, const uint64_t* a
     Csa<NB> cA, cX, cF;
     cF.template add<0>(f0);
     uint64_t anyA = 0, anyU = 0, anyR = 0, allA = ~0ull, allR = ~0ull;
-    uint32_t nA = 0, nU = 0, nf = (uint32_t)__popcll(f0 & val);
+    uint32_t nU = 0;
     static_for<0, L>([&](auto b) {
-        const uint64_t a = au[b()], u = au[L + b()] & ~a, x = a | u, f = inw[b() + 1];
+        const uint64_t a = au[b()], f = inw[b() + 1];
+        const uint64_t u = TIES ? au[L + b()] & ~a : 0ull, x = a | u;
         cA.template add<b()>(a);
-        cX.template add<b()>(x);
+        if constexpr (TIES) cX.template add<b()>(x);
         cF.template add<b() + 1>(f);
         anyA |= a & ~f;
-        anyU |= u & ~f;
+        if constexpr (TIES) anyU |= u & ~f;
         anyR |= ~(x | f);
         allA &= a | f;
         allR &= ~x | f;
-        nA += (uint32_t)__popcll(a & val);
-        nU += (uint32_t)__popcll(u & val);
-        nf += (uint32_t)__popcll(f & val);
+        if constexpr (TIES) nU += (uint32_t)__popcll(u & val);
     });
-    const uint64_t retreat = ~cX.template ge<L, K0 + 1>() | (orr & ~cX.template ge<L, K0 + 2>());
+    // per-trial counts as bit planes: the run totals are plane popcounts
+    uint64_t rA[NB], rF[NB];
+    cA.template resolve<0, L, false>(rA, 0);
+    cF.template resolve<0, N, false>(rF, 0);
+    uint32_t nA = 0, nf = 0;
+    static_for<0, NB>([&](auto i) {
+        nA += (uint32_t)__popcll(rA[i()] & val) << i();
+        nf += (uint32_t)__popcll(rF[i()] & val) << i();
+    });
+    const Csa<NB>& cXr = TIES ? cX : cA;
+    const uint64_t retreat = ~cXr.template ge<L, K0 + 1>() | (orr & ~cXr.template ge<L, K0 + 2>());
     const uint64_t attc = cA.template ge<L, needed>() | (ob & cA.template ge<L, needed - 1>());
     const uint64_t q1 = ~retreat & attc, q2 = ~retreat & ~attc;
-    const uint64_t agree = ~maj3(anyA, anyU, anyR);
+    const uint64_t agree = TIES ? ~maj3(anyA, anyU, anyR) : ~(anyA & anyR);
     const uint64_t appl = ~f0;
     const uint64_t valid = appl & ((ob & allA) | (~ob & allR));
     const uint64_t inb = (N > 3 * (int)ME) ? ~cF.template ge<N, (int)ME + 1>() : 0ull;
@@ -304,7 +315,7 @@ __device__ __forceinline__ void wave_epilogue(uint64_t* in0, const uint64_t* au0
         uint32_t dec = 0, out = 0;
         static_for<0, L>([&](auto b) {
             dec |= bit(au + b()) << (2 * b());
-            dec |= bit(au + L + b()) << (2 * b() + 1);
+            if constexpr (L % 2 == 0) dec |= bit(au + L + b()) << (2 * b() + 1);  // ties only at even L
         });
         static_for<0, 6>([&](auto k) { out |= bit(inw + k()) << k(); });
         if (live) {
@@ -459,25 +470,69 @@ struct Om3W {
     static constexpr int L = N - 1, S = N - 3, C = L - 1;
     static constexpr int W = 64 / C;               // trial words per wave task
     static constexpr int LANES = W * C;            // lanes busy in the subtree rounds
-    static constexpr int P = planes_c(L);          // root counter planes (L inputs)
     static constexpr int NIN = N + 3;
     static constexpr int CP = C + 1;               // padded R2T row (om3_round)
-    static constexpr int oIN = 0, oL0 = oIN + W * NIN, oR2 = oL0 + W * L, oRC = oR2 + W * C * CP;
-    static constexpr int end0 = oRC + W * L * P;
+    // IN[W][NIN] | L0[W][L] | R2T[W][C][CP] | R1T[W][L][L] (root inputs, receiver-major:
+    // R1T[w][j2][j1] = R1[j1, j2], L0[j2] on the diagonal) ; A/U roots reuse R2T
+    static constexpr int oIN = 0, oL0 = oIN + W * NIN, oR2 = oL0 + W * L, oR1 = oR2 + W * C * CP;
+    static constexpr int end0 = oR1 + W * L * L;
     static constexpr bool au_in_r2 = 2 * L <= C * CP;
     static constexpr int oAU = au_in_r2 ? oR2 : end0;
     static constexpr int words = ((au_in_r2 ? end0 : end0 + W * 2 * L) + 1) & ~1;
 };
 
+// Level 0 of a task's W words (one Philox per slot pair) into l0[w*L + j] and
+// the diagonal r1t[(w*L + j)*L + j] (root column j counts L0[j] as its own input).
+template <int N, int W>
+__device__ __forceinline__ void level0_r1t(const uint64_t* in0, uint64_t* l0, uint64_t* r1t,
+                                           uint32_t lane, uint64_t seed, uint64_t gw0) {
+    constexpr int L = N - 1, NIN = N + 3;
+    constexpr uint32_t NP0 = (L + 1) / 2;
+    for (uint32_t it = lane; it < (uint32_t)W * NP0; it += 64) {
+        const uint32_t w = it / NP0, p = it - w * NP0;
+        const uint64_t* in = in0 + w * NIN;
+        const uint64_t F0 = in[0], ob = in[N];
+        uint64_t lv[2];
+        lie_pair(seed, 0, p, gw0 + w, lv[0], lv[1]);
+        static_for<0, 2>([&](auto h) {
+            const uint32_t j = 2 * p + h();
+            if (j < (uint32_t)L) {
+                const uint64_t v = (F0 & lv[h()]) | (~F0 & ob);
+                l0[w * L + j] = v;
+                r1t[(w * L + j) * L + j] = v;
+            }
+        });
+    }
+}
+
+// Root majorities of W words from R1T (L contiguous inputs per column, a
+// compile-time carry-save count): strict majority attacks, a tie is
+// "undefined" (ba.py:188-195; only an even L ties).  au[w*2L + b] = A,
+// au[w*2L + L + b] = U.
+template <int L, int W>
+__device__ __forceinline__ void roots_r1t(const uint64_t* r1t0, uint64_t* au, uint32_t lane) {
+    for (uint32_t it = lane; it < (uint32_t)W * L; it += 64) {
+        const uint32_t w = it / L, col = it - w * L;
+        const uint64_t* r1t = r1t0 + (w * L + col) * L;
+        Csa<planes_c(L)> cnt;
+        static_for<0, L>([&](auto j) { cnt.template add<j()>(r1t[j()]); });
+        const uint64_t att = cnt.template ge<L, L / 2 + 1>();
+        au[w * 2 * L + col] = att;
+        if constexpr (L % 2 == 0) au[w * 2 * L + L + col] = cnt.template ge<L, L / 2>() & ~att;
+    }
+}
+
 // DIAG: lab-only ablation switches (tools/om3_lab.hip); the product uses 0.
-template <int N, int DIAG = 0>
+// STAGED: both inputs given (ba_gen_inputs_device buffers): the task's inputs
+// are loads and ballots only, the draw code is not compiled in.
+template <int N, int DIAG = 0, bool STAGED = false>
 __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
     uint64_t seed, GenSpec gs, uint64_t first_trial, uint64_t batch,
     const uint32_t* __restrict__ faulty, const uint8_t* __restrict__ order,
     uint64_t* __restrict__ decisions, uint8_t* __restrict__ outcome,
     uint64_t* __restrict__ counters, Sink sk) {
     using G = Om3W<N>;
-    constexpr int L = G::L, C = G::C, W = G::W, P = G::P, NIN = G::NIN;
+    constexpr int L = G::L, C = G::C, W = G::W, NIN = G::NIN;
     constexpr uint32_t ME = 3;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
@@ -497,10 +552,13 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
          task += (uint64_t)gridDim.x * wpb) {
         const uint64_t w0 = task * W;
         const uint64_t gw0 = (first_trial >> 6) + w0;
-        wave_inputs<N, W, DIAG>(img + G::oIN, lane, w0, seed, gs, first_trial, batch, faulty, order);
+        if constexpr (STAGED)
+            gen_words<N, W, -1>(img + G::oIN, lane, w0, seed, gs, first_trial, batch, faulty, order);
+        else
+            wave_inputs<N, W, DIAG>(img + G::oIN, lane, w0, seed, gs, first_trial, batch, faulty, order);
         __builtin_amdgcn_wave_barrier();
         FUSED_STAMP(0);
-        wave_level0<N, W, P>(img + G::oIN, img + G::oL0, img + G::oRC, lane, seed, gw0);
+        level0_r1t<N, W>(img + G::oIN, img + G::oL0, img + G::oR1, lane, seed, gw0);
         __builtin_amdgcn_wave_barrier();
         // ---- subtree rounds ------------------------------------------------------
         const uint64_t* in = img + G::oIN + lw * NIN;
@@ -510,12 +568,12 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
             const uint64_t r1 = om3_round<N>(in, act ? img[G::oL0 + lw * L + j1] : 0ull,
                                              img + G::oR2, lw, la, act, j1, seed, gw);
             FUSED_STAMP(1);
-            // root column j2 += R1[j1, b] (ripple add on the bit-sliced planes)
-            if (act) planes_add<P>(img + G::oRC + (lw * L + la + (la >= j1 ? 1u : 0u)) * P, r1);
-            __builtin_amdgcn_wave_barrier();
+            // R1[j1, b] is root input j1 of receiver column j2(b)
+            if (act) img[G::oR1 + (lw * L + la + (la >= j1 ? 1u : 0u)) * L + j1] = r1;
             FUSED_STAMP(2);
         }
-        wave_roots<L, W, P>(img + G::oRC, img + G::oAU, lane);
+        __builtin_amdgcn_wave_barrier();
+        roots_r1t<L, W>(img + G::oR1, img + G::oAU, lane);
         __builtin_amdgcn_wave_barrier();
         FUSED_STAMP(3);
         wave_epilogue<N, W, ME, DIAG>(img + G::oIN, img + G::oAU, lane, w0, batch, decisions,
@@ -565,7 +623,7 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
 constexpr int kQueueThreads = 512;  // 8 waves: two per SIMD
 constexpr int kQueueMaxTasks = 8;   // tasks a block holds in LDS at once
 
-template <int N>
+template <int N, int THREADS = kQueueThreads>
 struct Om3Q {
     static constexpr int L = N - 1, S = N - 3, C = L - 1, CP = C + 1;
     static constexpr int W = 64 / C;
@@ -574,7 +632,7 @@ struct Om3Q {
     static constexpr int tIN = 0, tL0 = W * NIN, tR1 = tL0 + W * L;
     static constexpr int task_words = ((tR1 + W * L * L) + 1) & ~1;
     static constexpr int wave_words = ((W * C * CP > W * 2 * L ? W * C * CP : W * 2 * L) + 1) & ~1;
-    static constexpr int waves = kQueueThreads / 64;
+    static constexpr int waves = THREADS / 64;
     static constexpr int lds_bytes = (kQueueMaxTasks * task_words + waves * wave_words) * 8;
 };
 
@@ -664,15 +722,40 @@ __device__ __forceinline__ void word_epilogue(const uint64_t* inw, const uint64_
     }
 }
 
+// Lab builds only (tools/om3q_lab.hip defines BA_QUEUE_STAMPS): per wave, the
+// s_memtime cycles spent in each phase and the units it took.  No output
+// depends on them.
+#ifdef BA_QUEUE_STAMPS
+__device__ unsigned long long g_q_stamps[4096][10];
+#define QSTAMP_INIT() unsigned long long qs_prev = __builtin_amdgcn_s_memtime(), qs_acc[10] = {0}
+#define QSTAMP(i)                                                   \
+    do {                                                            \
+        const unsigned long long qs_now = __builtin_amdgcn_s_memtime(); \
+        qs_acc[i] += qs_now - qs_prev;                              \
+        qs_prev = qs_now;                                           \
+    } while (0)
+#define QCOUNT(i) (qs_acc[i] += 1)
+#define QSTAMP_STORE()                                                                   \
+    if (lane == 0 && blockIdx.x * WAVES + wv < 4096)                                     \
+        for (int i = 0; i < 10; ++i) g_q_stamps[blockIdx.x * WAVES + wv][i] = qs_acc[i]
+#else
+#define QSTAMP_INIT()
+#define QSTAMP(i)
+#define QCOUNT(i)
+#define QSTAMP_STORE()
+#endif
+
 // STAGED: both inputs given (ba_gen_inputs_device buffers): loads only, the
-// draw code is not compiled in.
-template <int N, bool STAGED>
-__global__ __launch_bounds__(kQueueThreads, 2) void k_om3q(
+// draw code is not compiled in.  EPI: 1 = the epilogue as W word units (lane =
+// trial) in the queue; 0 = the bit-sliced epilogue of the whole task by the
+// wave that wrote its roots (lab A/B).
+template <int N, bool STAGED, int EPI = 1, int LAB = 0, int THREADS = kQueueThreads>
+__global__ __launch_bounds__(THREADS, THREADS / 256) void k_om3q(
     uint64_t seed, GenSpec gs, uint64_t first_trial, uint64_t batch,
     const uint32_t* __restrict__ faulty, const uint8_t* __restrict__ order,
     uint64_t* __restrict__ decisions, uint8_t* __restrict__ outcome,
     uint64_t* __restrict__ counters, Sink sk, uint32_t tasks_per_group) {
-    using G = Om3Q<N>;
+    using G = Om3Q<N, THREADS>;
     constexpr int L = G::L, C = G::C, W = G::W, NIN = G::NIN, WAVES = G::waves;
     constexpr uint32_t ME = 3;
     static_assert(G::W * G::L <= 128, "roots: two items per lane");
@@ -691,6 +774,7 @@ __global__ __launch_bounds__(kQueueThreads, 2) void k_om3q(
     const bool act = lane < (uint32_t)G::LANES;
     const uint32_t lw = act ? lw_ : 0;
     TrialCounts tc;
+    QSTAMP_INIT();
     for (uint64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
         const uint64_t t0 = grp * tasks_per_group;
         const uint32_t nt = (uint32_t)(ntasks - t0 < tasks_per_group ? ntasks - t0 : tasks_per_group);
@@ -715,8 +799,23 @@ __global__ __launch_bounds__(kQueueThreads, 2) void k_om3q(
             queue_level0<N, W>(timg + G::tIN, timg + G::tL0, timg + G::tR1, lane, seed,
                                (first_trial >> 6) + w0);
         }
+        QSTAMP(0);
         __syncthreads();
-        const uint32_t nunits = nt * (uint32_t)L, nepi = nt * (uint32_t)W;
+        QSTAMP(5);
+        const uint32_t nunits = nt * (uint32_t)L, nepi = EPI ? nt * (uint32_t)W : 0u;
+        // lab switches (tools/om3q_lab.hip; the product uses LAB = 0):
+        //   1: static units (wave v takes units v, v+8, ...), 2: s_setprio 1 for
+        //   waves 4-7, 4: waves 4-7 start phase B ~6k cycles late
+        if constexpr ((LAB & 2) != 0) {
+            if (wv >= WAVES / 2) __builtin_amdgcn_s_setprio(1);
+        }
+        if constexpr ((LAB & 4) != 0) {
+            if (wv >= WAVES / 2) {
+                __builtin_amdgcn_s_sleep(47);
+                __builtin_amdgcn_s_sleep(47);
+            }
+        }
+        uint32_t lab_next = wv;
         while (true) {
             // 1. an epilogue word unit of a task whose roots are written, if any
             uint32_t e = 0xFFFFFFFFu;
@@ -743,12 +842,19 @@ __global__ __launch_bounds__(kQueueThreads, 2) void k_om3q(
                 if (wg < total_words)
                     word_epilogue<N, ME>(timg + G::tIN + w * NIN, timg + G::tR1 + w * 2 * L, lane,
                                          wg * 64 + lane, batch, decisions, outcome, tc);
+                QSTAMP(3);
+                QCOUNT(8);
                 continue;
             }
             // 2. a round unit (task, j1), task-major
             uint32_t u = 0;
-            if (lane == 0) u = atomicAdd(&q_next, 1u);
-            u = __builtin_amdgcn_readfirstlane(u);
+            if constexpr ((LAB & 1) != 0) {
+                u = lab_next;
+                lab_next += WAVES;
+            } else {
+                if (lane == 0) u = atomicAdd(&q_next, 1u);
+                u = __builtin_amdgcn_readfirstlane(u);
+            }
             if (u < nunits) {
                 const uint32_t t = u / (uint32_t)L, j1 = u - t * (uint32_t)L;
                 uint64_t* timg = lds + t * G::task_words;
@@ -761,6 +867,8 @@ __global__ __launch_bounds__(kQueueThreads, 2) void k_om3q(
                 uint32_t d = 0;
                 if (lane == 0) d = atomicAdd(&q_done[t], 1u);
                 d = __builtin_amdgcn_readfirstlane(d);
+                QSTAMP(1);
+                QCOUNT(7);
                 if (d + 1 != (uint32_t)L) continue;
                 // the task's L-th round: its roots (compile-time carry-save counts of
                 // L contiguous R1T words, L0 on the diagonal; strict majority
@@ -788,6 +896,14 @@ __global__ __launch_bounds__(kQueueThreads, 2) void k_om3q(
                         timg[G::tR1 + w * 2 * L + L + col] = tie[k()];
                     }
                 });
+                QSTAMP(2);
+                if constexpr (EPI == 0) {
+                    __builtin_amdgcn_wave_barrier();
+                    wave_epilogue<N, W, ME, 0>(timg + G::tIN, timg + G::tR1, lane, (t0 + t) * W, batch,
+                                               decisions, outcome, tc);
+                    QSTAMP(3);
+                    continue;
+                }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 if (lane == 0) __hip_atomic_store(&e_ready[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 continue;
@@ -796,10 +912,15 @@ __global__ __launch_bounds__(kQueueThreads, 2) void k_om3q(
             //    task's rounds are still running and its word units will appear
             if (__hip_atomic_load(&e_claimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= nepi) break;
             __builtin_amdgcn_s_sleep(2);
+            QSTAMP(4);
         }
+        QSTAMP(4);
         __syncthreads();
+        QSTAMP(6);
     }
     block_flush<WAVES>(tc, lane, wv, counters, sk);
+    QSTAMP(6);
+    QSTAMP_STORE();
 }
 
 template <int N>
@@ -986,9 +1107,11 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om4w(
 
 // WAVE engine launch: one wave per W-word task, 4 independent waves per block,
 // at most two blocks per CU (two waves per SIMD, the kernels' register budget)
-// and a persistent task loop.
+// and a persistent task loop.  `staged` (optional) replaces `kernel` when both
+// inputs are given.
 template <typename G, typename K>
-inline hipError_t launch_wave(const RunArgs& a, K kernel, const char* name) {
+inline hipError_t launch_wave(const RunArgs& a, K kernel, const char* name, K staged = nullptr) {
+    if (staged && a.gen.faulty_mode == 0 && a.gen.order_mode == 0) kernel = staged;
     constexpr uint32_t wpb = kWaveThreads / 64;
     const uint64_t words = (a.batch + 63) / 64, tasks = (words + G::W - 1) / G::W;
     uint64_t blocks = (tasks + wpb - 1) / wpb;

@@ -14,9 +14,10 @@ bool wave_supported(const Geometry& g) {
 hipError_t launch_wave_engine(const RunArgs& a, const Geometry& g) {
     if (g.me == 4) return launch_wave4(a, g);
     if (g.me != 3) return hipErrorInvalidValue;
-    // depth 3: the queue kernel k_om3q; BA_WAVE_KIND=1 selects k_om3w (A/B, cross-checks)
+    // depth 3: k_om3w; BA_WAVE_KIND=2 selects the block-queue kernel k_om3q (A/B,
+    // cross-checks: DESIGN.md §4 on why the queue did not pay)
     const char* kind = getenv("BA_WAVE_KIND");
-    if (!(kind && kind[0] == '1')) {
+    if (kind && kind[0] == '2') {
         switch (g.n) {
 #define OM3Q_CASE(nn) \
     case nn: return launch_om3q<nn>(a);
@@ -28,7 +29,7 @@ hipError_t launch_wave_engine(const RunArgs& a, const Geometry& g) {
     }
     switch (g.n) {
 #define OM3W_CASE(nn) \
-    case nn: return launch_wave<Om3W<nn>>(a, k_om3w<nn>, "k_om3w");
+    case nn: return launch_wave<Om3W<nn>>(a, k_om3w<nn>, "k_om3w", k_om3w<nn, 0, true>);
         OM3W_CASE(5) OM3W_CASE(6) OM3W_CASE(7) OM3W_CASE(8) OM3W_CASE(9) OM3W_CASE(10)
         OM3W_CASE(11) OM3W_CASE(12) OM3W_CASE(13) OM3W_CASE(14)
 #undef OM3W_CASE

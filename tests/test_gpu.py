@@ -285,7 +285,7 @@ OM3_CASES = [(5, 3, 1, 1), (5, 4, 2, 1), (6, 3, 1, 2), (7, 3, 2, 1), (8, 3, 3, 1
 
 @pytest.mark.parametrize("n,m,f,fmode", OM3_CASES)
 def test_om3_wave_block_generic_vs_oracle(monkeypatch, n, m, f, fmode):
-    """k_om3q (default), k_om3w (BA_WAVE_KIND=1), k_fused3 (BA_FUSED_KIND=1) and
+    """k_om3w (default), k_om3q (BA_WAVE_KIND=2), k_fused3 (BA_FUSED_KIND=1) and
     k_fused (=2) against the oracle, over every synthetic-input path of the WAVE
     kernels' branch-free generator (f <= 2, 3, <= 6 and the generic fallback;
     random / exact / given faulty sets), a ragged batch, and the persistent
@@ -304,7 +304,7 @@ def test_om3_wave_block_generic_vs_oracle(monkeypatch, n, m, f, fmode):
                   L.ORDER_CONST, order_value=1, first_trial=64 * 77)
         ref = oracle_c.run(n, m, B, **kw)
     od, oo, ocnt = ref
-    for kind, cap, wk in (("0", None, "0"), ("0", "1", "0"), ("0", None, "1"), ("0", "1", "1"),
+    for kind, cap, wk in (("0", None, "0"), ("0", "1", "0"), ("0", None, "2"), ("0", "1", "2"),
                           ("1", None, "0"), ("2", None, "0")):
         monkeypatch.setenv("BA_FUSED_KIND", kind)
         monkeypatch.setenv("BA_WAVE_KIND", wk)
@@ -323,12 +323,16 @@ def test_om3_wave_block_generic_vs_oracle(monkeypatch, n, m, f, fmode):
         assert {k: res.counters[k] for k in ocnt} == ocnt, tag
 
 
+@pytest.mark.parametrize("kind", ["0", "2"])
 @pytest.mark.parametrize("n,B", [(10, 64 * 8 * 700 + 5), (13, 64 * 5 * 600 + 63), (7, 64 * 16 * 300)])
-def test_om3q_task_groups_vs_oracle(engine, n, B):
-    """k_om3q with several tasks per block group (tpg = ceil(tasks / CUs) = 2..3) and a
-    ragged last group, staged and drawn inputs, against the oracle."""
+def test_om3_mid_batches_vs_oracle(monkeypatch, engine, n, B, kind):
+    """Depth-3 WAVE kernels at mid-size batches: k_om3w (default: several tasks per
+    wave in its persistent loop) and k_om3q (BA_WAVE_KIND=2: several tasks per block
+    group, tpg = ceil(tasks / CUs) = 2..3, ragged last group), staged and drawn
+    inputs, against the oracle."""
     import torch
     from ba_amd import lib as L
+    monkeypatch.setenv("BA_WAVE_KIND", kind)
     kw = dict(seed=0xC0FFEE + n, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1,
               order_mode=L.ORDER_RANDOM, first_trial=64 * 11)
     od, oo, ocnt = oracle_c.run(n, 3, B, **kw)
