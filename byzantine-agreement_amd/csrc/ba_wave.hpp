@@ -564,7 +564,9 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
         const uint64_t* in = img + G::oIN + lw * NIN;
         const uint64_t gw = gw0 + lw;
         for (uint32_t j1 = 0; j1 < (uint32_t)L; ++j1) {
-            if constexpr ((DIAG & 8) == 0) wave_alternate_priority(j1);
+            // lab only: alternate the issue priority of the SIMD's two waves every
+            // round (round 1 default; round 2 measured it 2.5 us slower, om3_lab)
+            if constexpr ((DIAG & 8) != 0) wave_alternate_priority(j1);
             const uint64_t r1 = om3_round<N>(in, act ? img[G::oL0 + lw * L + j1] : 0ull,
                                              img + G::oR2, lw, la, act, j1, seed, gw);
             FUSED_STAMP(1);
