@@ -226,9 +226,16 @@ def main():
     fmax = L.default_fmax(n) if args.fmax < 0 else args.fmax
     engine_id = {"auto": L.ENGINE_AUTO, "fused": L.ENGINE_FUSED, "levels": L.ENGINE_LEVELS}[args.engine]
     eng = L.Engine(dev.index)
+    collective = None
     if world > 1:
         from ba_amd import dist as D
-        comm = D.init_comm(eng)
+        try:
+            comm = D.init_comm(eng)
+            collective = "rccl (libba_hip ba_comm_allreduce_device)"
+        except L.BAError as e:  # reported in the JSON line, never silent
+            print(f"bench: RCCL communicator failed ({e}); counters all-reduced over gloo",
+                  file=sys.stderr, flush=True)
+            collective = f"gloo fallback (RCCL failed: {e})"
     dec = torch.empty(B, dtype=torch.int64, device=dev)
     out = torch.empty(B, dtype=torch.uint8, device=dev)
     cnt = torch.zeros(16, dtype=torch.int64, device=dev)
@@ -304,6 +311,10 @@ def main():
         if comm is not None:
             comm.allreduce_device(cptr, stream=sp)  # the only collective: run counters (RCCL)
         torch.cuda.synchronize(dev)
+        if dist and comm is None:
+            host = cnt.cpu()
+            dist.all_reduce(host)
+            cnt.copy_(host)
         if dist:
             dist.barrier()
         wall = time.perf_counter() - t0
@@ -398,6 +409,7 @@ def main():
                                    f"random order, decisions+outcome written",
                        "n": n, "m": m, "trials_per_gpu_step": B, "engine": args.engine,
                        "parallelism": f"trial-dp{world}"},
+            "collective": collective,
             "inputs": "in-kernel Philox draws" if args.inputs_in_kernel else
                       "staged in HBM before the timed region (ba_gen_inputs_device); lies drawn in-kernel",
             "ms_per_step_gpu_events": round(gpu_ms / args.steps, 4),
