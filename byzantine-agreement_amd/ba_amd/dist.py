@@ -89,12 +89,13 @@ def run_instance_split(comm: L.Comm, params: L.Params, batch: int, device: torch
 class InstanceSplitGraphs:
     """The first-hop split with its launch sequence captured in hipGraphs.
 
-    A config-5 call (n=16, m=5) is ~15 kernels, most of them small, so at small
+    A config-5 call (n=16, m=5) is 6-10 kernels, most of them small, so at small
     batches the launch gaps cost about as much as the work.  The local halves of
     the split are captured once per (params, batch) and replayed: with one rank
-    the whole call is one graph; with N ranks graph 1 = this rank's subtree votes
-    into its rows of the full vote array, then the C-ABI vote all-gather (RCCL,
-    eager), then graph 2 = root majorities + quorum.  The graphs run on their own
+    (which owns every subtree) the call is the unsplit pass, one graph; with N
+    ranks graph 1 = this rank's subtree votes into its rows of the full vote
+    array, then the C-ABI vote all-gather (RCCL, eager), then graph 2 = root
+    majorities + quorum.  The graphs run on their own
     Engine (ctx): the device buffers they captured (scratch, counter sink) can
     never be regrown under them by another caller of a shared ctx.  Outputs are
     the same tensors on every replay (overwritten); results equal the eager split
@@ -121,15 +122,17 @@ class InstanceSplitGraphs:
         # initialisation on the current stream
         self.stream.wait_stream(torch.cuda.current_stream(device))
         with torch.cuda.stream(self.stream):
-            self._tree()
-            self._gather()
-            self._root()
+            if self.world == 1:
+                self._whole()
+            else:
+                self._tree()
+                self._gather()
+                self._root()
         torch.cuda.synchronize(device)
-        if self.world == 1:  # no collective: one graph for the whole call
+        if self.world == 1:  # one rank, no collective: the unsplit pass as one graph
             self.g_tree = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_tree, stream=self.stream):
-                self._tree()
-                self._root()
+                self._whole()
             self.g_root = None
         else:
             self.g_tree = torch.cuda.CUDAGraph()
@@ -144,6 +147,12 @@ class InstanceSplitGraphs:
             self.engine.subtree_votes_device(self.params, self.batch, self.jb, self.je,
                                              self.votes[self.jb * (self.params.n - 2):].data_ptr(),
                                              stream=self.stream.cuda_stream)
+
+    def _whole(self):
+        self.cnt.zero_()
+        self.engine.run_device(self.params, self.batch, d_decisions=self.dec.data_ptr(),
+                               d_outcome=self.out.data_ptr(), d_counters=self.cnt.data_ptr(),
+                               stream=self.stream.cuda_stream)
 
     def _gather(self):
         if self.world > 1:

@@ -20,6 +20,32 @@ __device__ __forceinline__ uint32_t grid_threads() { return gridDim.x * kBlock; 
 // ---------------------------------------------------------------------------
 // input bit-slicing: one wave per 64-trial word
 // ---------------------------------------------------------------------------
+// The planes of word w (lane = trial): F[g] for the n generals, OB (order is
+// attack), OO (order is "other"), VAL (trial of the batch); lane g < n returns
+// F[g] in `mine`, every lane returns ob / oo / vv.
+__device__ __forceinline__ void word_inputs(uint32_t n, uint64_t seed, const GenSpec& gs, uint64_t t0,
+                                            uint64_t ntrials, const uint32_t* __restrict__ faulty,
+                                            const uint8_t* __restrict__ order, uint64_t w,
+                                            uint32_t lane, uint64_t& mine, uint64_t& ob,
+                                            uint64_t& oo, uint64_t& vv) {
+    const uint64_t i = w * 64 + lane;  // trial index within the chunk
+    const bool valid = i < ntrials;
+    uint32_t fm = 0, oc = 0;
+    if (valid) {
+        if (gs.faulty_mode == 0) fm = faulty[i];
+        if (gs.order_mode == 0) oc = order[i];
+        gen_trial(n, seed, gs, t0 + i, fm, oc);
+    }
+    mine = 0;
+    for (uint32_t g = 0; g < n; ++g) {
+        const uint64_t b = __ballot(valid && ((fm >> g) & 1u));
+        if (lane == g) mine = b;
+    }
+    ob = __ballot(valid && oc == 1);
+    oo = __ballot(valid && oc == 2);
+    vv = __ballot(valid);
+}
+
 __global__ __launch_bounds__(kBlock) void k_input(uint32_t n, uint64_t seed, GenSpec gs,
                                                   uint64_t t0, uint64_t ntrials,
                                                   const uint32_t* __restrict__ faulty,
@@ -31,22 +57,8 @@ __global__ __launch_bounds__(kBlock) void k_input(uint32_t n, uint64_t seed, Gen
     const uint64_t words_per_grid = (uint64_t)gridDim.x * (kBlock / 64);
     for (uint64_t w = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); w < W;
          w += words_per_grid) {
-        const uint64_t i = w * 64 + lane;  // trial index within the chunk
-        const bool valid = i < ntrials;
-        uint32_t fm = 0, oc = 0;
-        if (valid) {
-            if (gs.faulty_mode == 0) fm = faulty[i];
-            if (gs.order_mode == 0) oc = order[i];
-            gen_trial(n, seed, gs, t0 + i, fm, oc);
-        }
-        uint64_t mine = 0;
-        for (uint32_t g = 0; g < n; ++g) {
-            const uint64_t b = __ballot(valid && ((fm >> g) & 1u));
-            if (lane == g) mine = b;
-        }
-        const uint64_t ob = __ballot(valid && oc == 1);
-        const uint64_t oo = __ballot(valid && oc == 2);
-        const uint64_t vv = __ballot(valid);
+        uint64_t mine, ob, oo, vv;
+        word_inputs(n, seed, gs, t0, ntrials, faulty, order, w, lane, mine, ob, oo, vv);
         if (lane < n) scratch[offF + (uint64_t)lane * W + w] = mine;
         if (lane == 0) {
             scratch[offOB + w] = ob;
@@ -264,20 +276,57 @@ struct TopPlan {
     FastDiv D[kTopMax + 1];            // D[k] = prod_{i=k+1..K} (L - i): level-K slots per level-k slot
 };
 
+// Inputs fused in (IN.fuse, batches of at most kTopFuseWords words): every block
+// bit-slices the batch's inputs itself into LDS (a wave per word) and reads F /
+// OB from there, and block 0 also stores them to scratch for the later kernels
+// -- one launch (k_input) less on the latency-bound small batches of config 5.
+constexpr uint32_t kTopFuseWords = 32;
+struct TopInputs {
+    uint32_t fuse, n;
+    uint64_t seed, t0, ntrials;
+    GenSpec gs;
+    const uint32_t* faulty;
+    const uint8_t* order;
+    uint64_t offOO, offVAL;
+};
+
 __global__ __launch_bounds__(kBlock) void k_relay_top(TopPlan tp, FastDiv divW, uint32_t work,
                                                       uint64_t seed, uint64_t gw0,
                                                       const uint8_t* __restrict__ sender,
                                                       uint64_t* __restrict__ scratch,
-                                                      uint64_t offF, uint64_t offOB) {
+                                                      uint64_t offF, uint64_t offOB, TopInputs IN) {
     const uint32_t W = divW.d;
     const uint32_t work0 = tp.np0 * W;
     const uint64_t* F = scratch + offF;
+    const uint64_t* OBp = scratch + offOB;
+    __shared__ uint64_t sIn[kTopFuseWords * (kMaxN + 1)];  // F[g][w] rows, then OB[w]
+    if (IN.fuse) {
+        const uint32_t lane = threadIdx.x & 63;
+        for (uint32_t w = threadIdx.x >> 6; w < W; w += kBlock / 64) {
+            uint64_t mine, ob, oo, vv;
+            word_inputs(IN.n, IN.seed, IN.gs, IN.t0, IN.ntrials, IN.faulty, IN.order, w, lane, mine,
+                        ob, oo, vv);
+            if (lane < IN.n) sIn[lane * W + w] = mine;
+            if (lane == 0) sIn[IN.n * W + w] = ob;
+            if (blockIdx.x == 0) {
+                if (lane < IN.n) scratch[offF + (uint64_t)lane * W + w] = mine;
+                if (lane == 0) {
+                    scratch[offOB + w] = ob;
+                    scratch[IN.offOO + w] = oo;
+                    scratch[IN.offVAL + w] = vv;
+                }
+            }
+        }
+        __syncthreads();
+        F = sIn;
+        OBp = sIn + IN.n * W;
+    }
     for (uint32_t idx = blockIdx.x * kBlock + threadIdx.x; idx < work; idx += grid_threads()) {
         if (idx < work0) {  // level 0, whole: commander -> lieutenant x (ba.py:263-277)
             const uint32_t p = fdiv(idx, divW), w = idx - p * W;
             uint64_t lie[2];
             lie_pair(seed, 0, p, gw0 + w, lie[0], lie[1]);
-            const uint64_t f0 = F[w], ob = scratch[offOB + w];
+            const uint64_t f0 = F[w], ob = OBp[w];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const uint32_t x = 2 * p + h;
@@ -291,7 +340,7 @@ __global__ __launch_bounds__(kBlock) void k_relay_top(TopPlan tp, FastDiv divW, 
         const uint32_t pairK = (tp.xbK >> 1) + pl;
         uint64_t lieK[2];
         lie_pair(seed, tp.K, pairK, gw, lieK[0], lieK[1]);
-        const uint64_t ob = scratch[offOB + w];
+        const uint64_t ob = OBp[w];
         uint32_t prev_parent = 0xFFFFFFFFu;
         uint64_t parent_val = 0;
         for (int h = 0; h < 2; ++h) {
@@ -586,13 +635,28 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
     const uint64_t W = (ntrials + 63) / 64;
     const uint64_t gw0 = (a.first_trial + trial0) / 64;
     hipStream_t st = a.stream;
-    { ProfScope ps(a.prof, "k_input", st);
-    hipLaunchKernelGGL(k_input, dim3(blocks_for(W * 64, 4096)), dim3(kBlock), 0, st, a.n, a.seed,
-                       a.gen, a.first_trial + trial0, ntrials,
-                       a.faulty ? a.faulty + trial0 : nullptr, a.order ? a.order + trial0 : nullptr,
-                       scratch, W, lay.F, lay.OB, lay.OO, lay.VAL); }
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    // small batches: the inputs are bit-sliced inside k_relay_top (TopInputs)
+    const bool no_fuse_in = getenv("BA_NO_INPUT_FUSION") && atoi(getenv("BA_NO_INPUT_FUSION")) != 0;
+    TopInputs tin{};
+    tin.fuse = (!no_fuse_in && W <= kTopFuseWords && a.n <= (uint32_t)kMaxN) ? 1u : 0u;
+    tin.n = a.n;
+    tin.seed = a.seed;
+    tin.t0 = a.first_trial + trial0;
+    tin.ntrials = ntrials;
+    tin.gs = a.gen;
+    tin.faulty = a.faulty ? a.faulty + trial0 : nullptr;
+    tin.order = a.order ? a.order + trial0 : nullptr;
+    tin.offOO = lay.OO;
+    tin.offVAL = lay.VAL;
+    hipError_t e = hipSuccess;
+    if (!tin.fuse) {
+        ProfScope ps(a.prof, "k_input", st);
+        hipLaunchKernelGGL(k_input, dim3(blocks_for(W * 64, 4096)), dim3(kBlock), 0, st, a.n, a.seed,
+                           a.gen, a.first_trial + trial0, ntrials,
+                           a.faulty ? a.faulty + trial0 : nullptr, a.order ? a.order + trial0 : nullptr,
+                           scratch, W, lay.F, lay.OB, lay.OO, lay.VAL);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     // where level k / majority p live: scratch, except the level-1 child
     // results (R_1, or L_1 at depth 1) that a subtree pass leaves in votes_out
     auto Lptr = [&](uint32_t k) -> uint64_t* {
@@ -614,6 +678,13 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
     static const bool no_top = getenv("BA_NO_TOP_RELAY") && atoi(getenv("BA_NO_TOP_RELAY")) != 0;
     const uint32_t kf = (lay.leaf_fused || !job.tree || g.me == 0) ? ktop : g.me - 1;
     uint32_t k_first = 0;
+    if (tin.fuse && (no_top || kf > (uint32_t)kTopMax)) {  // no k_relay_top: inputs on their own
+        ProfScope ps(a.prof, "k_input", st);
+        hipLaunchKernelGGL(k_input, dim3(blocks_for(W * 64, 4096)), dim3(kBlock), 0, st, a.n, a.seed,
+                           a.gen, a.first_trial + trial0, ntrials, tin.faulty, tin.order, scratch, W,
+                           lay.F, lay.OB, lay.OO, lay.VAL);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     if (!no_top && kf <= (uint32_t)kTopMax) {
         TopPlan tp{};
         tp.K = kf;
@@ -634,7 +705,7 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
         ProfScope ps(a.prof, "k_relay_top", st);
         hipLaunchKernelGGL(k_relay_top, dim3(blocks_for(work, 16384)), dim3(kBlock), 0, st, tp,
                            make_fastdiv((uint32_t)W), work, a.seed, gw0, d_sender, scratch, lay.F,
-                           lay.OB);
+                           lay.OB, tin);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         k_first = kf + 1;
     }

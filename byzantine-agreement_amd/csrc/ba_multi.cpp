@@ -312,6 +312,12 @@ extern "C" int ba_run_instance_split_multi(struct ba_ctx* ctx, struct ba_comm* c
     const uint64_t slots = local == BA_OK ? ba_vote_slots(n, p->m, 0, n - 1) : 0;
     if (local == BA_OK && slots == 0)
         local = failf(BA_ENOTSUP, "OM(0) has no relay subtrees (n=%u, m=%u)", n, p->m);
+    if (comm->nranks == 1) {  // one rank owns every subtree: the unsplit pass, no vote array
+        if (local == BA_OK && batch > 0)
+            local = ba_run_trials_device(ctx, p, batch, d_faulty_mask, d_order, nullptr, nullptr,
+                                         d_decisions, d_outcome, comm->d_cnt, comm->stream);
+        return finish_job(comm, local, counters_out, false);
+    }
     const uint64_t W = (batch + 63) / 64;
     const size_t need = (size_t)(slots * W * sizeof(uint64_t));
     if (local == BA_OK && need > comm->votes_bytes) {

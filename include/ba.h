@@ -256,7 +256,8 @@ int ba_comm_allgather_votes_device(struct ba_comm* comm, uint32_t n, uint32_t m,
  *   first-hop subtree -- subtree votes, vote all-gather, root majorities and
  *   quorum; decisions / outcome (batch entries) and counters_out identical on
  *   every rank and equal to an unsplit ba_run_trials on the same params
- *   (LEVELS engine, Philox lies, given or drawn inputs). */
+ *   (Philox lies, given or drawn inputs).  With one rank the rank owns every
+ *   subtree and the call is the unsplit pass itself. */
 int ba_run_trials_multi(struct ba_ctx* ctx, struct ba_comm* comm, const ba_params* p,
                         uint64_t total_trials, uint64_t* d_decisions, uint8_t* d_outcome,
                         ba_counters* counters_out, uint64_t* share_first,

@@ -514,3 +514,32 @@ def test_run_trials_multi_world1_rccl(engine):
         assert ei.value.code == L.EINVAL
     finally:
         comm.close()
+
+
+@pytest.mark.parametrize("n,m,B", [(16, 5, 100), (10, 3, 64 * 32), (10, 3, 64 * 32 + 1), (7, 2, 5),
+                                   (13, 4, 64 * 20 + 9)])
+def test_levels_input_fusion_vs_oracle(monkeypatch, n, m, B):
+    """LEVELS with the inputs bit-sliced inside k_relay_top (batches up to 32 words)
+    and with the separate k_input launch (BA_NO_INPUT_FUSION=1, and above 32 words):
+    both equal the oracle, for drawn and given inputs."""
+    from ba_amd import lib as L
+    kw = dict(seed=0xFACE + n, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1,
+              order_mode=L.ORDER_RANDOM, first_trial=64 * 9)
+    od, oo, ocnt = oracle_c.run(n, m, B, **kw)
+    rng = np.random.default_rng(B)
+    fm = rng.integers(0, 1 << n, B, dtype=np.uint64).astype(np.uint32)
+    oc = rng.choice([0, 1, 2], B).astype(np.uint8)
+    gd, go, gcnt = oracle_c.run(n, m, B, seed=3, faulty=fm, order=oc)
+    for off in ("0", "1"):
+        monkeypatch.setenv("BA_NO_INPUT_FUSION", off)
+        e = L.Engine(0)
+        try:
+            res = e.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
+            same(res.decisions, od, f"drawn, no_fusion={off}")
+            same(res.outcome, oo, f"drawn, no_fusion={off}")
+            assert {k: res.counters[k] for k in ocnt} == ocnt
+            res = e.run(n, m, B, seed=3, faulty=fm, order=oc, engine=L.ENGINE_LEVELS)
+            same(res.decisions, gd, f"given, no_fusion={off}")
+            assert {k: res.counters[k] for k in gcnt} == gcnt
+        finally:
+            e.close()
