@@ -1,6 +1,6 @@
 """ba.py's command surface over libba_hip.
 
-    python -m ba_amd.repl N [--seed S] [--om M]
+    python -m ba_amd.repl N [--seed S] [--om M] [--timed [--gap SEC]]
 
 Commands and output formats are ba.py's (ba.py:354-445):
   actual-order <o>          every general's majority, then the quorum line
@@ -10,6 +10,11 @@ Each `actual-order` is one batch=1 ba_run_trials call; the generals run
 ba.py's canonical schedule (one election tick before every command), so with
 --seed S the output equals `random.seed(S)` + ba.py under that schedule.
 --om M > 1 runs OM(M) rounds (Philox lies) instead of ba.py's OM(1).
+--timed replaces that schedule by ba.py's own timing on a virtual clock
+(ba_amd.timing: 0.1 s run-loop ticks, heartbeat, election, wait_majority):
+commands arrive --gap seconds apart (the first --gap after start-up), or at
+"@T <command>" (absolute seconds),
+so e.g. a g-state at t=0 shows every general as secondary, as ba.py does.
 Differences from ba.py: no threads, sockets or sleeps; EOF ends the loop
 instead of raising EOFError (ba.py:367).
 """
@@ -19,6 +24,7 @@ import argparse
 import sys
 
 from .generals import Cluster
+from .timing import TimedCluster, run_timed
 
 
 def execute(cluster: Cluster, line: str, out) -> bool:
@@ -67,14 +73,31 @@ def run(cluster: Cluster, lines, out=sys.stdout):
             break
 
 
+def timed_lines(lines, gap: float):
+    """(arrival time, command) pairs: "@T cmd" arrives at T, others gap after
+    the previous command (the first one gap after start-up)."""
+    t = gap
+    for line in lines:
+        if line.startswith("@"):
+            stamp, _, line = line[1:].partition(" ")
+            t = float(stamp)
+        yield t, line
+        t += gap
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(prog="ba_amd.repl", description=__doc__.split("\n\n")[0])
     ap.add_argument("N", type=int, help="generals at start (ba.py:12)")
     ap.add_argument("--seed", type=int, default=None, help="random.seed() of ba.py's RNG")
     ap.add_argument("--om", type=int, default=1, help="OM depth (1 = ba.py)")
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--timed", action="store_true", help="ba.py's tick timing (ba_amd.timing)")
+    ap.add_argument("--gap", type=float, default=1.0, help="seconds between commands (--timed)")
     a = ap.parse_args(argv)
-    cluster = Cluster(a.N, seed=a.seed, om=a.om, device=a.device)
+    if a.timed:
+        cluster = TimedCluster(a.N, seed=a.seed, om=a.om, device=a.device)
+    else:
+        cluster = Cluster(a.N, seed=a.seed, om=a.om, device=a.device)
 
     def lines():
         while True:
@@ -83,7 +106,10 @@ def main(argv=None):
             except EOFError:
                 return
 
-    run(cluster, lines())
+    if a.timed:
+        run_timed(cluster, timed_lines(lines(), a.gap), sys.stdout, execute)
+    else:
+        run(cluster, lines())
 
 
 if __name__ == "__main__":
