@@ -125,7 +125,7 @@ bool plan_fused(const Geometry& g, FusedPlan& fp);
 hipError_t launch_leaf(const Geometry& g, uint64_t seed, uint64_t gw0, uint32_t W,
                        uint32_t srbase, uint32_t srcnt, uint32_t lbase, const uint64_t* Lm2,
                        const uint8_t* d_sender, const uint64_t* F, const uint64_t* d_members,
-                       uint64_t* Rm1, hipStream_t st, Prof* prof);
+                       uint64_t* Rm1, bool up, hipStream_t st, Prof* prof);
 hipError_t launch_fused(const RunArgs& a, const Geometry& g, bool plan_ok, const FusedPlan& fp,
                         const FusedPlan* d_fp, const uint8_t* d_sender, uint64_t* partials);
 

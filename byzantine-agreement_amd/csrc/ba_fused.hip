@@ -65,6 +65,73 @@ __global__ __launch_bounds__(256) void k_leaf(uint32_t me, uint64_t seed, uint64
     }
 }
 
+// LEVELS leaf-up (me >= 3): the S+1 sibling leaf blocks rho.x (x < G = S+1,
+// the children of one level me-3 slot rho) of one word run on G lanes of one
+// wave, and the wave also takes the next majority up,
+//     R_{me-2}[rho.x] = maj(L_{me-2}[rho.x], R_{me-1}[rho.a.x] : a != x)
+// (G inputs, inner tie -> non-attack).  Receiver x's inputs sit in the OTHER
+// blocks' columns (member d of block a is sibling d + (d >= a)), so the lanes
+// swap them through LDS, receiver-major T[x][a] with L_{me-2}[rho.x] on the
+// diagonal, as the WAVE kernels' om3_round does for R1.  R_{me-1} is never
+// stored: one k_majority launch and the S words per block it read go away.
+// A unit = (rho, word), GPW = 64 / G units per wave; slot rho.x = srbase +
+// unit's rho rank * G + x (the level me-2 range starts at its first child).
+template <int S>
+__global__ __launch_bounds__(256) void k_leaf_up(uint32_t me, uint64_t seed, uint64_t gw0,
+                                                 FastDiv divW, uint32_t units, uint32_t srbase,
+                                                 uint32_t lbase, const uint64_t* __restrict__ Lm2,
+                                                 const uint8_t* __restrict__ snd2,
+                                                 const uint64_t* __restrict__ F,
+                                                 const uint64_t* __restrict__ members,
+                                                 uint64_t* __restrict__ Rm2) {
+    constexpr int G = S + 1, GP = G + 1, GPW = 64 / G, NPD = (S + 1) / 2;
+    __shared__ uint64_t tr[4][GPW][G][GP];  // [wave][unit][receiver x][sender a], rows padded
+    const uint32_t W = divW.d;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t g = lane / G, x = lane - g * G;
+    const bool act = g < (uint32_t)GPW;
+    const uint32_t gg = act ? g : 0;
+    for (uint32_t u0 = blockIdx.x * 4 * GPW; u0 < units; u0 += gridDim.x * 4 * GPW) {
+        const uint32_t u = u0 + wv * GPW + gg;
+        const bool ok = act && u < units;
+        const uint32_t rl = fdiv(ok ? u : 0u, divW);
+        const uint32_t w = (ok ? u : 0u) - rl * W;
+        const uint32_t sl = rl * G + x;
+        const uint32_t sr = srbase + sl;
+        uint64_t par = 0;
+        if (ok) {
+            const uint64_t gw = gw0 + w;
+            const uint64_t mem = members[sr];
+            par = Lm2[(uint64_t)(sr - lbase) * W + w];
+            const uint64_t fs = F[(uint64_t)snd2[sr] * W + w];
+            const uint32_t x0 = sr * (uint32_t)S;
+            uint64_t lw[2 * NPD];
+            lie_pairs<NPD>(seed, me - 1, x0 >> 1, gw, lw);
+            const uint64_t oddmask = 0ull - (uint64_t)(x0 & 1u);
+            uint64_t diag[S], Fm[S], R[S];
+            static_for<0, S>([&](auto a) {
+                uint64_t lie;
+                if constexpr (S % 2 == 1) lie = lw[a()] ^ ((lw[a()] ^ lw[a() + 1]) & oddmask);
+                else lie = lw[a()];
+                diag[a()] = (fs & lie) | (~fs & par);
+                Fm[a()] = F[((mem >> (5 * a())) & 31u) * W + w];
+            });
+            leaf_block<S>(me, seed, gw, sr, diag, Fm, R);
+            uint64_t* t = &tr[wv][gg][0][x];
+            t[x * GP] = par;
+            static_for<0, S>([&](auto d) { t[(d() + (d() >= x ? 1u : 0u)) * GP] = R[d()]; });
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (ok) {
+            const uint64_t* col = &tr[wv][gg][x][0];
+            Csa<planes_c(G)> cnt;
+            static_for<0, G>([&](auto a) { cnt.template add<a()>(col[a()]); });
+            Rm2[(uint64_t)sl * W + w] = cnt.template ge<G, G / 2 + 1>();
+        }
+        __builtin_amdgcn_wave_barrier();  // tr is rewritten by the next unit
+    }
+}
+
 // ---------------------------------------------------------------------------
 // FUSED: one block per group of WPB trial words, everything in LDS
 // ---------------------------------------------------------------------------
@@ -482,26 +549,38 @@ template <int S>
 static void launch_leaf_s(uint32_t me, uint64_t seed, uint64_t gw0, uint32_t W, uint32_t work,
                           uint32_t srbase, uint32_t lbase, const uint64_t* Lm2,
                           const uint8_t* snd2, const uint64_t* F, const uint64_t* mem,
-                          uint64_t* Rm1, hipStream_t st) {
+                          uint64_t* Rout, bool up, hipStream_t st) {
+    if (up) {  // work = units (rho, word); GPW units per wave, 4 waves per block
+        constexpr uint32_t GPW = 64 / (S + 1);
+        uint64_t b = (work + 4 * GPW - 1) / (4 * GPW);
+        if (b > 16384) b = 16384;
+        if (b < 1) b = 1;
+        hipLaunchKernelGGL(k_leaf_up<S>, dim3((uint32_t)b), dim3(256), 0, st, me, seed, gw0,
+                           make_fastdiv(W), work, srbase, lbase, Lm2, snd2, F, mem, Rout);
+        return;
+    }
     uint64_t b = (work + 255) / 256;
     if (b > 16384) b = 16384;
     if (b < 1) b = 1;
     hipLaunchKernelGGL(k_leaf<S>, dim3((uint32_t)b), dim3(256), 0, st, me, seed, gw0,
-                       make_fastdiv(W), work, srbase, lbase, Lm2, snd2, F, mem, Rm1);
+                       make_fastdiv(W), work, srbase, lbase, Lm2, snd2, F, mem, Rout);
 }
 
 hipError_t launch_leaf(const Geometry& g, uint64_t seed, uint64_t gw0, uint32_t W,
                        uint32_t srbase, uint32_t srcnt, uint32_t lbase, const uint64_t* Lm2,
                        const uint8_t* d_sender, const uint64_t* F, const uint64_t* d_members,
-                       uint64_t* Rm1, hipStream_t st, Prof* prof) {
-    ProfScope ps(prof, "k_leaf", st);
+                       uint64_t* Rm1, bool up, hipStream_t st, Prof* prof) {
+    ProfScope ps(prof, up ? "k_leaf_up" : "k_leaf", st);
+    if (up && g.me < 3) return hipErrorInvalidValue;  // R_{me-2} would be the root level
     const uint32_t S = g.n - g.me;
-    const uint32_t work = (uint32_t)((uint64_t)srcnt * W);
+    if (up && srcnt % (S + 1) != 0) return hipErrorInvalidValue;  // whole sibling groups only
+    // work items: (leaf block, word), or (sibling group, word) for leaf-up
+    const uint32_t work = (uint32_t)((uint64_t)(up ? srcnt / (S + 1) : srcnt) * W);
     if (work == 0) return hipSuccess;
     const uint8_t* snd2 = d_sender + g.sender_off[g.me - 2];  // last general of each level me-2 slot
     switch (S) {
 #define LEAF_CASE(s) \
-    case s: launch_leaf_s<s>(g.me, seed, gw0, W, work, srbase, lbase, Lm2, snd2, F, d_members, Rm1, st); break;
+    case s: launch_leaf_s<s>(g.me, seed, gw0, W, work, srbase, lbase, Lm2, snd2, F, d_members, Rm1, up, st); break;
         LEAF_CASE(2) LEAF_CASE(3) LEAF_CASE(4) LEAF_CASE(5) LEAF_CASE(6) LEAF_CASE(7)
         LEAF_CASE(8) LEAF_CASE(9) LEAF_CASE(10) LEAF_CASE(11) LEAF_CASE(12)
 #undef LEAF_CASE

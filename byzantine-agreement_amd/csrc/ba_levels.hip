@@ -482,108 +482,6 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(uint32_t n, uint32_t me, ui
 }
 
 // ---------------------------------------------------------------------------
-// Fused tail for small batches (config 5's latency path): the inner majority
-// levels pmax..1 and the root + quorum epilogue of ONE trial word per block,
-// the upper levels' results kept in LDS.  Replaces pmax k_majority launches
-// and the k_epilogue launch (each a latency-bound ~3-6 us kernel at one word
-// plus its launch gap) by one launch.  Same arithmetic as k_majority /
-// k_epilogue: strict majorities, inner tie -> non-attack, root tie ->
-// undefined (ba.py:159-195), quorum / IC flags by trial_result (ba.py:197-255).
-// LDS: R_p for p = 1..pmax (lvl_off[p] words each level), then A / U / F / OB /
-// OO / VAL of the word.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kTailThreads = 1024;
-constexpr uint64_t kTailMaxWords = 64;
-constexpr uint32_t kTailMaxSlots = 4096;  // largest level held in LDS
-struct TailPlan {
-    uint32_t pmax, L;
-    uint32_t S[kFusedMaxDepth + 1];        // level sizes
-    uint64_t offL[kFusedMaxDepth + 1];     // scratch offset of L_p, p = 0..pmax
-    uint64_t offC;                         // scratch offset of R_{pmax+1} (the children of pmax)
-    uint32_t lds[kFusedMaxDepth + 1];      // LDS offset of R_p, p = 1..pmax
-    uint32_t ldsA;                         // A[L] U[L] F[n] OB OO VAL
-};
-
-__global__ __launch_bounds__(kTailThreads) void k_tail(TailPlan tp, uint32_t n, uint32_t me, uint64_t W,
-                                                       const uint64_t* __restrict__ scratch,
-                                                       uint64_t offF, uint64_t offOB, uint64_t offOO,
-                                                       uint64_t offVAL, uint64_t* __restrict__ decisions,
-                                                       uint8_t* __restrict__ outcome,
-                                                       uint64_t* __restrict__ counters, Sink sk) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
-    const uint64_t w = blockIdx.x;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, L = tp.L;
-    // inner majorities, level pmax down to 1: R_p[y] over L_p[y] and s-1 children
-    for (int p = (int)tp.pmax; p >= 1; --p) {
-        const uint32_t s = L - (uint32_t)p;
-        const uint32_t thr = s / 2 + 1;
-        const uint64_t* Lp = scratch + tp.offL[p];
-        const bool cg = p == (int)tp.pmax;  // children in HBM (R_{pmax+1}) or in LDS
-        const uint64_t* Cg = scratch + tp.offC;
-        const uint64_t* Cs = sm + tp.lds[p + 1 <= (int)tp.pmax ? p + 1 : p];
-        for (uint32_t y = tid; y < tp.S[p]; y += kTailThreads) {
-            const uint32_t sr = y / s, b = y - sr * s;
-            Count<5> cnt;
-            cnt.add(Lp[(uint64_t)y * W + w]);
-            for (uint32_t a0 = 0; a0 < s; a0 += kLoadChunk) {  // a chunk's loads in flight together
-                uint64_t v[kLoadChunk];
-#pragma unroll
-                for (uint32_t q = 0; q < kLoadChunk; ++q) {
-                    const uint32_t a = a0 + q;
-                    const uint64_t cs = ((uint64_t)sr * s + a) * (s - 1) + (b - (b > a));
-                    v[q] = (a >= s || a == b) ? 0ull : (cg ? Cg[cs * W + w] : Cs[cs]);
-                }
-#pragma unroll
-                for (uint32_t q = 0; q < kLoadChunk; ++q) cnt.add(v[q]);
-            }
-            sm[tp.lds[p] + y] = cnt.ge(thr);
-        }
-        __syncthreads();
-    }
-    // roots (lanes b < L of wave 0) and the word's input planes
-    uint64_t* sA = sm + tp.ldsA;
-    uint64_t* sU = sA + L;
-    uint64_t* sF = sU + L;
-    if (tid < 64) {
-        if (lane < L) {
-            const uint32_t b = lane;
-            Count<5> cnt;
-            cnt.add(scratch[tp.offL[0] + (uint64_t)b * W + w]);
-            const uint64_t* R1 = sm + tp.lds[1];
-            for (uint32_t a = 0; a < L; ++a)
-                if (a != b) cnt.add(R1[a * (L - 1) + b - (b > a)]);
-            const uint64_t att = cnt.ge(L / 2 + 1);
-            sA[b] = att;
-            sU[b] = (L & 1u) ? 0ull : (cnt.ge(L / 2) & ~att);
-        }
-        if (lane < n) sF[lane] = scratch[offF + (uint64_t)lane * W + w];
-        if (lane == 0) {
-            sF[n] = scratch[offOB + w];
-            sF[n + 1] = scratch[offOO + w];
-            sF[n + 2] = scratch[offVAL + w];
-        }
-    }
-    __syncthreads();
-    TrialCounts tc;
-    if (tid < 64 && ((sF[n + 2] >> lane) & 1ull)) {
-        uint32_t A = 0, U = 0, fm = 0;
-        for (uint32_t b = 0; b < L; ++b) {
-            A |= (uint32_t)((sA[b] >> lane) & 1ull) << (b + 1);
-            U |= (uint32_t)((sU[b] >> lane) & 1ull) << (b + 1);
-        }
-        for (uint32_t g = 0; g < n; ++g) fm |= (uint32_t)((sF[g] >> lane) & 1ull) << g;
-        const uint32_t ob = (uint32_t)(sF[n] >> lane) & 1u, oo = (uint32_t)(sF[n + 1] >> lane) & 1u;
-        uint64_t dec;
-        uint32_t out;
-        finish_trial(n, me, fm, oo ? 2u : ob, A, U, dec, out, tc);
-        const uint64_t i = w * 64 + lane;
-        if (decisions) decisions[i] = dec;
-        if (outcome) outcome[i] = (uint8_t)out;
-    }
-    block_counts_sink<kTailThreads>(tc, counters, sk);
-}
-
-// ---------------------------------------------------------------------------
 // ba.py OM(1) in its canonical draw order (lie table), one thread per trial
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_table(uint32_t n, uint32_t relay, uint32_t me,
@@ -825,6 +723,11 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
                            a.seed, gw0, Lprev, Lptr(k), scratch + lay.F, snd);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
+    // leaf-up (me >= 3): k_leaf also takes the majority of level me-2 from its
+    // block's S column results, so R_{me-1} is never stored and the inner
+    // majority launches start one level higher.  BA_NO_LEAF_UP=1: off (A/B).
+    const bool no_up = getenv("BA_NO_LEAF_UP") && atoi(getenv("BA_NO_LEAF_UP")) != 0;
+    const bool leaf_up = job.tree && lay.leaf_fused && g.me >= 3 && !no_up;
     if (job.tree && lay.leaf_fused) {  // L_{me-1} and L_me on the fly: R_{me-1} from L_{me-2}
         // leaf blocks = slots of level me-2; level 0 is stored whole, but its
         // subtree range is the first-hop lieutenants [jb, je) themselves
@@ -832,21 +735,14 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
         const uint32_t srbase = top ? lay.jb : (uint32_t)lay.base[g.me - 2];
         const uint32_t srcnt = top ? lay.je - lay.jb : (uint32_t)lay.cnt[g.me - 2];
         e = launch_leaf(g, a.seed, gw0, (uint32_t)W, srbase, srcnt, (uint32_t)lay.base[g.me - 2],
-                        Lptr(g.me - 2), d_sender, scratch + lay.F, a.members, Rptr(g.me - 1), st,
-                        a.prof);
+                        Lptr(g.me - 2), d_sender, scratch + lay.F, a.members,
+                        leaf_up ? Rptr(g.me - 2) : Rptr(g.me - 1), leaf_up, st, a.prof);
         if (e != hipSuccess) return e;
     }
-    // small batches of whole trees: the upper majority levels and the epilogue
-    // in one k_tail launch (pmax = the deepest level whose slots fit its LDS)
-    const int pdeep = job.tree ? (int)g.me - (lay.leaf_fused ? 2 : 1) : 0;
-    const bool no_tail = getenv("BA_NO_TAIL_FUSION") && atoi(getenv("BA_NO_TAIL_FUSION")) != 0;
-    int pmax = 0;
-    if (!no_tail && job.tree && job.root && !job.votes_out && lay.jb == 0 && lay.je == g.L &&
-        W <= kTailMaxWords && g.me >= 1 && g.me <= (uint32_t)kFusedMaxDepth - 1 && pdeep >= 1) {
-        for (int p = 1; p <= pdeep && g.S[p] <= kTailMaxSlots; ++p) pmax = p;
-    }
-    // inner majorities, bottom-up (levels me-1..1, or me-2..1 after k_leaf), down to pmax+1
-    for (int p = pdeep; p >= pmax + 1; --p) {
+    // inner majorities, bottom-up: levels me-1..1 (no leaf fusion), me-2..1
+    // (k_leaf wrote R_{me-1}) or me-3..1 (k_leaf wrote R_{me-2})
+    const int pdeep = job.tree ? (int)g.me - (lay.leaf_fused ? (leaf_up ? 3 : 2) : 1) : 0;
+    for (int p = pdeep; p >= 1; --p) {
         const uint32_t s = g.L - (uint32_t)p;
         const uint32_t work = (uint32_t)(lay.cnt[p] * W);
         const uint32_t ybase = (uint32_t)lay.base[p], cbase = (uint32_t)lay.base[p + 1];
@@ -864,29 +760,6 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (!job.root) return hipSuccess;
-    if (pmax >= 1) {  // k_tail: levels pmax..1, roots, quorum, counters
-        TailPlan tp{};
-        tp.pmax = (uint32_t)pmax;
-        tp.L = g.L;
-        uint32_t off = 0;
-        for (int p = 0; p <= pmax; ++p) {
-            tp.S[p] = (uint32_t)g.S[p];
-            tp.offL[p] = lay.Lk[p];
-            if (p >= 1) {
-                tp.lds[p] = off;
-                off += (uint32_t)g.S[p];
-            }
-        }
-        tp.offC = (pmax + 1 == (int)g.me) ? lay.Lk[pmax + 1] : lay.Rp[pmax + 1];
-        tp.ldsA = off;
-        const size_t lds = (size_t)(off + 2 * g.L + g.n + 3) * 8;
-        uint64_t* dec = a.decisions ? a.decisions + trial0 : nullptr;
-        uint8_t* out = a.outcome ? a.outcome + trial0 : nullptr;
-        ProfScope ps(a.prof, "k_tail", st);
-        hipLaunchKernelGGL(k_tail, dim3((uint32_t)W), dim3(kTailThreads), lds, st, tp, a.n, a.me, W,
-                           scratch, lay.F, lay.OB, lay.OO, lay.VAL, dec, out, a.counters, a.sink);
-        return hipGetLastError();
-    }
     // root + quorum epilogue over L_0 and the level-1 child results
     const uint64_t* C1 = job.votes_in ? job.votes_in
                          : (g.me >= 2 ? scratch + lay.Rp[1] : (g.me == 1 ? scratch + lay.Lk[1] : nullptr));

@@ -519,11 +519,11 @@ def test_run_trials_multi_world1_rccl(engine):
 @pytest.mark.parametrize("n,m,B", [(16, 5, 100), (16, 5, 1), (10, 3, 64 * 64), (10, 3, 64 * 64 + 1),
                                    (7, 2, 5), (13, 4, 64 * 20 + 9), (9, 5, 130)])
 def test_levels_small_batch_fusions_vs_oracle(monkeypatch, n, m, B):
-    """LEVELS small-batch fusions on and off -- the inputs bit-sliced inside
-    k_relay_top (batches up to 2 words) vs the k_input launch, and the k_tail
-    launch (upper majority levels + epilogue per word, batches up to 64 words)
-    vs k_majority + k_epilogue (BA_NO_INPUT_FUSION / BA_NO_TAIL_FUSION = 1):
-    every combination equals the oracle, for drawn and given inputs."""
+    """LEVELS launch fusions on and off -- the inputs bit-sliced inside
+    k_relay_top (batches up to 2 words) vs the k_input launch, and k_leaf taking
+    the level me-2 majority itself (leaf-up, m_eff >= 3) vs writing R_{me-1} for
+    a k_majority launch (BA_NO_INPUT_FUSION / BA_NO_LEAF_UP = 1): every
+    combination equals the oracle, for drawn and given inputs."""
     from ba_amd import lib as L
     kw = dict(seed=0xFACE + n, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1,
               order_mode=L.ORDER_RANDOM, first_trial=64 * 9)
@@ -532,10 +532,10 @@ def test_levels_small_batch_fusions_vs_oracle(monkeypatch, n, m, B):
     fm = rng.integers(0, 1 << n, B, dtype=np.uint64).astype(np.uint32)
     oc = rng.choice([0, 1, 2], B).astype(np.uint8)
     gd, go, gcnt = oracle_c.run(n, m, B, seed=3, faulty=fm, order=oc)
-    for off_in, off_tail in (("0", "0"), ("1", "1"), ("0", "1"), ("1", "0")):
-        off = off_in + off_tail
+    for off_in, off_up in (("0", "0"), ("1", "1"), ("0", "1"), ("1", "0")):
+        off = off_in + off_up
         monkeypatch.setenv("BA_NO_INPUT_FUSION", off_in)
-        monkeypatch.setenv("BA_NO_TAIL_FUSION", off_tail)
+        monkeypatch.setenv("BA_NO_LEAF_UP", off_up)
         e = L.Engine(0)
         try:
             res = e.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
