@@ -224,8 +224,21 @@ struct ba_ctx {
 
 // A call about to use the ctx's scratch / sink on stream `s` first waits for
 // the ctx's previous call if that ran on another stream (include/ba.h: calls of
-// one ctx may come from any streams; the library orders them itself).  Skipped
-// while `s` is capturing a graph: the replay's ordering is the caller's.
+// one ctx may come from any streams; the library orders them itself).  The
+// ordering event is recorded on the previous call's stream only at that switch:
+// it then follows everything queued there, the previous call included.  A
+// record after EVERY call would cost every call's stream ~1.3-3 us before its
+// next kernel (tools/marker_cost.hip: +3.0 us per launch for a DisableTiming
+// event, +1.3 us without the system-scope fence; bench.py 1M trials 59.8 ->
+// 57.0 us per step without it), which the single-stream case never needs.
+// Skipped while `s` is capturing a graph: the replay's ordering is the caller's.
+// The ctx's own stream (it lives as long as the ctx).  Library-internal: the
+// communicators of ba_multi.cpp run their whole jobs on it, so the stream the
+// ctx's ordering may record on never dies before the ctx does.
+extern "C" __attribute__((visibility("hidden"))) hipStream_t ba_ctx_stream_internal(ba_ctx* ctx) {
+    return ctx->stream;
+}
+
 static bool stream_capturing(hipStream_t s) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
@@ -233,17 +246,16 @@ static bool stream_capturing(hipStream_t s) {
 
 static hipError_t ctx_order(ba_ctx* ctx, hipStream_t s) {
     if (!ctx->have_last || ctx->last_stream == s || stream_capturing(s)) return hipSuccess;
-    return hipStreamWaitEvent(s, ctx->last_ev, 0);
+    hipError_t e = hipEventRecord(ctx->last_ev, ctx->last_stream);
+    return e == hipSuccess ? hipStreamWaitEvent(s, ctx->last_ev, 0) : e;
 }
 
 static hipError_t ctx_mark(ba_ctx* ctx, hipStream_t s) {
-    if (stream_capturing(s)) return hipSuccess;
-    hipError_t e = hipEventRecord(ctx->last_ev, s);
-    if (e == hipSuccess) {
+    if (!stream_capturing(s)) {
         ctx->last_stream = s;
         ctx->have_last = true;
     }
-    return e;
+    return hipSuccess;
 }
 
 namespace ba {
@@ -254,7 +266,7 @@ hipEvent_t Prof::take() {
         return e;
     }
     hipEvent_t e = nullptr;
-    (void)hipEventCreate(&e);
+    (void)hipEventCreateWithFlags(&e, hipEventReleaseToDevice);  // timing only: no system-scope fence
     return e;
 }
 void Prof::begin(const char* name, hipStream_t s) {

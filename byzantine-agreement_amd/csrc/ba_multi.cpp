@@ -97,8 +97,11 @@ struct ba_comm {
     uint64_t* d_cnt = nullptr;  // BA_NCOUNTERS uint64 on the device, all-reduced in place
     uint64_t* d_votes = nullptr;  // full vote array of the split (grown on demand)
     size_t votes_bytes = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;  // the ctx's own stream (not owned: the ctx outlives the comm)
 };
+
+// ba_api.cpp, library-internal
+extern "C" hipStream_t ba_ctx_stream_internal(struct ba_ctx* ctx);
 
 extern "C" int ba_comm_unique_id(unsigned char id[BA_COMM_ID_BYTES]) {
     if (!id) return failf(BA_EINVAL, "id is NULL");
@@ -127,9 +130,11 @@ extern "C" int ba_comm_create(struct ba_ctx* ctx, int nranks, int rank,
     c->nranks = nranks;
     c->rank = rank;
     c->device = dev;
-    if (hipMalloc(&c->d_cnt, BA_NCOUNTERS * sizeof(uint64_t)) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-        if (c->d_cnt) (void)hipFree(c->d_cnt);
+    // whole jobs run on the ctx's own stream: a ctx call on another stream
+    // afterwards orders itself after it by an event recorded on that stream
+    // (ba_api.cpp ctx_order), so the stream must live as long as the ctx
+    c->stream = ba_ctx_stream_internal(ctx);
+    if (hipMalloc(&c->d_cnt, BA_NCOUNTERS * sizeof(uint64_t)) != hipSuccess) {
         delete c;
         return failf(BA_ENOMEM, "communicator buffers");
     }
@@ -137,7 +142,6 @@ extern "C" int ba_comm_create(struct ba_ctx* ctx, int nranks, int rank,
     memcpy(&u, id, BA_COMM_ID_BYTES);
     const ncclResult_t e = r.comm_init_rank(&c->comm, nranks, u, rank);
     if (e != ncclSuccess) {
-        (void)hipStreamDestroy(c->stream);
         (void)hipFree(c->d_cnt);
         delete c;
         return failf(BA_EDEVICE, "ncclCommInitRank(%d ranks, rank %d): %s", nranks, rank,
@@ -152,7 +156,6 @@ extern "C" void ba_comm_destroy(struct ba_comm* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm && rccl().h) (void)rccl().comm_destroy(c->comm);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->d_cnt) (void)hipFree(c->d_cnt);
     if (c->d_votes) (void)hipFree(c->d_votes);
     delete c;

@@ -18,8 +18,10 @@
  *     the device scratch it allocates inside the ctx (including the run
  *     counter reduction slots).  Calls of one ctx may be made on different
  *     streams: the library orders each call after the ctx's previous one
- *     (an event on the previous call's stream), except while the stream is
- *     capturing a graph -- a graph replay's ordering is the caller's.  Device
+ *     (an event it records on the previous call's stream when the stream
+ *     changes), except while the stream is capturing a graph -- a graph
+ *     replay's ordering is the caller's.  So a stream that carried a call of
+ *     a ctx must stay valid until that ctx's next call or ba_ctx_destroy.  Device
  *     buffers a captured graph holds stay valid until the ctx grows its
  *     scratch for a LARGER call: give a graph its own ctx.
  *
@@ -208,10 +210,11 @@ int ba_root_from_votes_device(struct ba_ctx* ctx, const ba_params* p, uint64_t b
  * One process per GPU.  Rank 0 calls ba_comm_unique_id and ships the
  * BA_COMM_ID_BYTES bytes to every rank out of band (MPI, a socket, a file, a
  * torch.distributed store); every rank calls ba_comm_create on its ctx (the
- * communicator owns an RCCL communicator, a counter buffer, a vote buffer and
- * a stream).  RCCL is opened at run time (librccl.so.1, or the copy already
- * loaded in the process).  Every rank of a comm must make the same sequence
- * of collective calls with the same params. */
+ * communicator owns an RCCL communicator, a counter buffer and a vote buffer,
+ * and runs its whole jobs on the ctx's own stream; destroy a comm before its
+ * ctx).  RCCL is opened at run time (librccl.so.1, or the copy already loaded
+ * in the process).  Every rank of a comm must make the same sequence of
+ * collective calls with the same params. */
 #define BA_COMM_ID_BYTES 128
 struct ba_comm;
 int ba_ctx_device(struct ba_ctx* ctx, int* device);
