@@ -40,6 +40,8 @@ __host__ __device__ __forceinline__ uint64_t maj3(uint64_t a, uint64_t b, uint64
     return (uint64_t)maj3_32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) << 32 |
            maj3_32((uint32_t)a, (uint32_t)b, (uint32_t)c);
 }
+__host__ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return xor3_32(a, b, c); }
+__host__ __device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) { return maj3_32(a, b, c); }
 
 // ---------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al., SC'11).  The key is kernel-uniform, so the key
@@ -239,32 +241,32 @@ struct Count {
 // Count<P>::add.  Which levels are occupied after K inputs is a function of K
 // alone, so every branch below is resolved at compile time.
 // ---------------------------------------------------------------------------
-template <int NL>
+template <int NL, typename T = uint64_t>
 struct Csa {
-    uint64_t acc[NL], pend[NL];
+    T acc[NL], pend[NL];
 
     // push the (N+1)-th event into level L
     template <int L, int N>
-    __host__ __device__ __forceinline__ void push(uint64_t e) {
+    __host__ __device__ __forceinline__ void push(T e) {
         static_assert(L < NL, "Csa: too few levels for this many inputs");
         if constexpr (N == 0) {
             acc[L] = e;
         } else if constexpr (N % 2 == 1) {
             pend[L] = e;
         } else {
-            const uint64_t a = acc[L], p = pend[L];
+            const T a = acc[L], p = pend[L];
             acc[L] = xor3(a, p, e);
             push<L + 1, (N - 2) / 2>(maj3(a, p, e));
         }
     }
     // add the (K+1)-th input
     template <int K>
-    __host__ __device__ __forceinline__ void add(uint64_t x) {
+    __host__ __device__ __forceinline__ void add(T x) {
         push<0, K>(x);
     }
     // binary digits r[0..NL) of the count after N events at level L (+ carry in)
     template <int L, int N, bool CIN>
-    __host__ __device__ __forceinline__ void resolve(uint64_t (&r)[NL], uint64_t cin) const {
+    __host__ __device__ __forceinline__ void resolve(T (&r)[NL], T cin) const {
         if constexpr (L < NL) {
             constexpr bool hasA = N >= 1, hasP = N >= 2 && N % 2 == 0;
             constexpr int up = N >= 1 ? (N - 1) / 2 : 0;  // events level L passed up
@@ -276,8 +278,8 @@ struct Csa {
                 r[L] = hasA ? acc[L] : (hasP ? pend[L] : cin);
                 resolve<L + 1, up, false>(r, 0);
             } else if constexpr (terms == 2) {
-                const uint64_t x = hasA ? acc[L] : pend[L];
-                const uint64_t y = CIN ? cin : pend[L];
+                const T x = hasA ? acc[L] : pend[L];
+                const T y = CIN ? cin : pend[L];
                 r[L] = x ^ y;
                 resolve<L + 1, up, true>(r, x & y);
             } else {
@@ -286,18 +288,18 @@ struct Csa {
             }
         }
     }
-    // lanes whose count (after K inputs) is >= T
-    template <int K, int T>
-    __host__ __device__ __forceinline__ uint64_t ge() const {
-        if constexpr (T <= 0) return ~0ull;
-        else if constexpr (T > K) return 0ull;
+    // lanes whose count (after K inputs) is >= TH
+    template <int K, int TH>
+    __host__ __device__ __forceinline__ T ge() const {
+        if constexpr (TH <= 0) return (T)~(T)0;
+        else if constexpr (TH > K) return (T)0;
         else {
-            uint64_t r[NL];
+            T r[NL];
             resolve<0, K, false>(r, 0);
-            uint64_t gt = 0, eq = ~0ull;
+            T gt = 0, eq = (T)~(T)0;
 #pragma unroll
             for (int i = NL - 1; i >= 0; --i) {
-                if ((T >> i) & 1) {
+                if ((TH >> i) & 1) {
                     eq &= r[i];
                 } else {
                     gt |= eq & r[i];

@@ -129,6 +129,83 @@ __device__ __forceinline__ void gen_words(uint64_t* in0, uint32_t lane, uint64_t
     });
 }
 
+// Staged inputs (both given, e.g. ba_gen_inputs_device buffers) of words
+// [0, W) of a wave task -> bit-sliced words in LDS, in0[w*(N+3) + g].  Every
+// lane packs its trial's faulty bits, order bits and live bit into one dword
+// (bits 0..N-1 F, N OB, N+1 OO, N+2 VAL); plane g is one ballot (an SGPR
+// pair) that v_writelane drops into lane g of a VGPR pair (writelane4), and
+// lanes g < N+3 store their plane with one LDS write.  Against gen_words<.., -1> (a ballot
+// per plane, then a lane-select of every ballot in every lane) this is ~60
+// instead of ~140 instructions per word, and it keeps no ballot live across
+// words (the old code's SGPRs spilled to VGPR lanes).  All 2W loads are issued
+// before the first use.
+// Lanes G0..G0+CNT-1 of the VGPR pair (lo, hi) = the uniform 64-bit values
+// b[0..CNT) (v_writelane_b32; clang has no writelane builtin here).  The
+// ballots that produced b are VALU writes of SGPRs, and v_writelane reads its
+// data SGPR early: without wait states between them a GPU run got wrong planes
+// (the hazard recognizer cannot see into the asm), so each group of up to 4
+// planes pays one s_nop 4 after its ballots.
+template <int G0, int CNT>
+__device__ __forceinline__ void writelane4(uint32_t& lo, uint32_t& hi, const uint64_t (&b)[4]) {
+    const uint32_t l0 = (uint32_t)b[0], h0 = (uint32_t)(b[0] >> 32), l1 = (uint32_t)b[1],
+                   h1 = (uint32_t)(b[1] >> 32), l2 = (uint32_t)b[2], h2 = (uint32_t)(b[2] >> 32),
+                   l3 = (uint32_t)b[3], h3 = (uint32_t)(b[3] >> 32);
+    if constexpr (CNT == 4)
+        asm volatile("s_nop 4\n\tv_writelane_b32 %0, %2, %10\n\tv_writelane_b32 %1, %3, %10\n\t"
+                     "v_writelane_b32 %0, %4, %11\n\tv_writelane_b32 %1, %5, %11\n\t"
+                     "v_writelane_b32 %0, %6, %12\n\tv_writelane_b32 %1, %7, %12\n\t"
+                     "v_writelane_b32 %0, %8, %13\n\tv_writelane_b32 %1, %9, %13"
+                     : "+v"(lo), "+v"(hi)
+                     : "s"(l0), "s"(h0), "s"(l1), "s"(h1), "s"(l2), "s"(h2), "s"(l3), "s"(h3),
+                       "i"(G0), "i"(G0 + 1), "i"(G0 + 2), "i"(G0 + 3));
+    else if constexpr (CNT == 3)
+        asm volatile("s_nop 4\n\tv_writelane_b32 %0, %2, %8\n\tv_writelane_b32 %1, %3, %8\n\t"
+                     "v_writelane_b32 %0, %4, %9\n\tv_writelane_b32 %1, %5, %9\n\t"
+                     "v_writelane_b32 %0, %6, %10\n\tv_writelane_b32 %1, %7, %10"
+                     : "+v"(lo), "+v"(hi)
+                     : "s"(l0), "s"(h0), "s"(l1), "s"(h1), "s"(l2), "s"(h2), "i"(G0), "i"(G0 + 1),
+                       "i"(G0 + 2));
+    else if constexpr (CNT == 2)
+        asm volatile("s_nop 4\n\tv_writelane_b32 %0, %2, %6\n\tv_writelane_b32 %1, %3, %6\n\t"
+                     "v_writelane_b32 %0, %4, %7\n\tv_writelane_b32 %1, %5, %7"
+                     : "+v"(lo), "+v"(hi)
+                     : "s"(l0), "s"(h0), "s"(l1), "s"(h1), "i"(G0), "i"(G0 + 1));
+    else
+        asm volatile("s_nop 4\n\tv_writelane_b32 %0, %2, %4\n\tv_writelane_b32 %1, %3, %4"
+                     : "+v"(lo), "+v"(hi)
+                     : "s"(l0), "s"(h0), "i"(G0));
+    (void)l1; (void)h1; (void)l2; (void)h2; (void)l3; (void)h3;
+}
+
+template <int N, int W>
+__device__ __forceinline__ void stage_words(uint64_t* in0, uint32_t lane, uint64_t w0, uint64_t batch,
+                                            const uint32_t* __restrict__ faulty,
+                                            const uint8_t* __restrict__ order) {
+    constexpr int NIN = N + 3;
+    constexpr uint32_t FMASK = N >= 32 ? 0xFFFFFFFFu : ((1u << N) - 1u);
+    uint32_t fm[W], oc[W];
+    static_for<0, W>([&](auto q) {
+        const uint64_t i = (w0 + q()) * 64 + lane;
+        const bool v = i < batch;
+        fm[q()] = v ? faulty[i] : 0u;
+        oc[q()] = v ? (uint32_t)order[i] : 0u;
+    });
+    static_for<0, W>([&](auto q) {
+        const uint32_t c = oc[q()];
+        const bool v = (w0 + q()) * 64 + lane < batch;
+        const uint32_t x = (fm[q()] & FMASK) | (c == 1u ? 1u << N : 0u) | (c == 2u ? 2u << N : 0u) |
+                           (v ? 4u << N : 0u);
+        uint32_t lo = 0, hi = 0;
+        static_for<0, (NIN + 3) / 4>([&](auto grp) {
+            constexpr int g0 = 4 * grp();
+            uint64_t b[4];
+            static_for<0, 4>([&](auto j) { b[j()] = g0 + j() < NIN ? __ballot((x >> (g0 + j())) & 1u) : 0ull; });
+            writelane4<g0, (NIN - g0 < 4 ? NIN - g0 : 4)>(lo, hi, b);
+        });
+        if (lane < (uint32_t)NIN) in0[q() * NIN + lane] = (uint64_t)hi << 32 | lo;
+    });
+}
+
 // ---------------------------------------------------------------------------
 // Pieces shared by the WAVE kernels (one wave resolves a task of W words).
 // ---------------------------------------------------------------------------
@@ -142,7 +219,7 @@ __device__ __forceinline__ void wave_inputs(uint64_t* in0, uint32_t lane, uint64
     constexpr int NIN = N + 3;
     const uint32_t pk = gs.faulty_mode == 0 ? 0u : (gs.f < (uint32_t)N ? gs.f : (uint32_t)N);
     if (gs.faulty_mode == 0 && gs.order_mode == 0) {  // staged inputs: loads only
-        gen_words<N, W, -1>(in0, lane, w0, seed, gs, first_trial, batch, faulty, order);
+        stage_words<N, W>(in0, lane, w0, batch, faulty, order);
     } else if constexpr ((DIAG & 16) != 0) {  // lab: near-free stand-in inputs
         static_for<0, W>([&](auto wq) {
             const uint64_t h = (w0 + wq() + 1) * 0x9E3779B97F4A7C15ull;
@@ -209,35 +286,47 @@ __device__ __forceinline__ void wave_roots(const uint64_t* rc, uint64_t* au, uin
 
 // Quorum epilogue of W words in two phases (ba.py:206-262, restated per trial
 // by trial_result in ba_device.hpp, which the oracle test pins):
-//  1. lane = word: the whole decision is bit-sliced over the word's 64 trials
-//     -- compile-time carry-save counts of attacks / non-retreats / faulty
-//     generals against the quorum thresholds, ORs and ANDs over the loyal
-//     lieutenants for agreement and validity -- and the run counters are
-//     popcounts of the resulting planes masked by the live-trial word.  The
-//     six outcome planes overwrite the word's faulty planes in LDS.
+//  1. lane = (word, byte): the whole decision is bit-sliced over 8 trials of
+//     one word -- byte k of every plane -- with compile-time carry-save counts
+//     of attacks / non-retreats / faulty generals against the quorum
+//     thresholds, ORs and ANDs over the loyal lieutenants for agreement and
+//     validity; the run counters are popcounts of the resulting planes masked
+//     by the live-trial bits.  The six outcome planes overwrite the word's
+//     faulty planes in LDS (byte k each).  Every operation is bitwise, so a
+//     word splits into 8 independent byte lanes: 8 words x 8 bytes = one
+//     instruction stream for the whole task, where lane = word left 56 of 64
+//     lanes idle through ~380 instructions of 64-bit (two-half) operations.
 //  2. lane = trial: the 2L decision bits and 6 outcome bits of each word are
 //     picked out of the 32-bit half holding this lane (one bfe + one shift-or
 //     per bit) and stored.
 // Per trial this is ~3x fewer instructions than running trial_result in every
 // lane, which needed all 2L+N+3 bits gathered first.
-template <int N, uint32_t ME>
-__device__ __forceinline__ void epilogue_planes(uint64_t* inw, const uint64_t* au,
-                                                TrialCounts& tc) {
+// epilogue_core: plane p of the inputs is in(p) (F[0..N), OB, OO, VAL), root
+// planes au(b) (A[0..L), U[0..L)), outcome plane k is written by out(k, v);
+// T is the slice type (uint64_t: a whole word; uint32_t: one byte of it).
+template <typename T>
+__device__ __forceinline__ uint32_t popc_t(T x) {
+    if constexpr (sizeof(T) == 8) return (uint32_t)__popcll(x);
+    else return (uint32_t)__popc(x);
+}
+
+template <int N, uint32_t ME, typename T, typename In, typename Au, typename Out>
+__device__ __forceinline__ void epilogue_core(In in, Au au, Out out, TrialCounts& tc) {
     constexpr int L = N - 1, NB = planes_c(N);
     // an odd number of root inputs never ties: no undefined decisions, U == 0
     constexpr bool TIES = L % 2 == 0;
     constexpr int needed = N == 1 ? 1 : (N <= 3 ? N - 1 : 2 * ((N - 1) / 3) + 1);
     constexpr int K0 = L - needed;  // retreat: #(A|U) <= K0 (+1 when the commander retreats)
-    const uint64_t val = inw[N + 2], oo = inw[N + 1];
-    const uint64_t ob = inw[N] & ~oo, orr = ~inw[N] & ~oo;  // commander attack / retreat
-    const uint64_t f0 = inw[0];
-    Csa<NB> cA, cX, cF;
+    const T val = in(N + 2), oo = in(N + 1);
+    const T ob = in(N) & ~oo, orr = ~in(N) & ~oo;  // commander attack / retreat
+    const T f0 = in(0);
+    Csa<NB, T> cA, cX, cF;
     cF.template add<0>(f0);
-    uint64_t anyA = 0, anyU = 0, anyR = 0, allA = ~0ull, allR = ~0ull;
+    T anyA = 0, anyU = 0, anyR = 0, allA = (T)~(T)0, allR = (T)~(T)0;
     uint32_t nU = 0;
     static_for<0, L>([&](auto b) {
-        const uint64_t a = au[b()], f = inw[b() + 1];
-        const uint64_t u = TIES ? au[L + b()] & ~a : 0ull, x = a | u;
+        const T a = au(b()), f = in(b() + 1);
+        const T u = TIES ? au(L + b()) & ~a : (T)0, x = a | u;
         cA.template add<b()>(a);
         if constexpr (TIES) cX.template add<b()>(x);
         cF.template add<b() + 1>(f);
@@ -246,43 +335,58 @@ __device__ __forceinline__ void epilogue_planes(uint64_t* inw, const uint64_t* a
         anyR |= ~(x | f);
         allA &= a | f;
         allR &= ~x | f;
-        if constexpr (TIES) nU += (uint32_t)__popcll(u & val);
+        if constexpr (TIES) nU += popc_t<T>(u & val);
     });
     // per-trial counts as bit planes: the run totals are plane popcounts
-    uint64_t rA[NB], rF[NB];
+    T rA[NB], rF[NB];
     cA.template resolve<0, L, false>(rA, 0);
     cF.template resolve<0, N, false>(rF, 0);
     uint32_t nA = 0, nf = 0;
     static_for<0, NB>([&](auto i) {
-        nA += (uint32_t)__popcll(rA[i()] & val) << i();
-        nf += (uint32_t)__popcll(rF[i()] & val) << i();
+        nA += popc_t<T>(rA[i()] & val) << i();
+        nf += popc_t<T>(rF[i()] & val) << i();
     });
-    const Csa<NB>& cXr = TIES ? cX : cA;
-    const uint64_t retreat = ~cXr.template ge<L, K0 + 1>() | (orr & ~cXr.template ge<L, K0 + 2>());
-    const uint64_t attc = cA.template ge<L, needed>() | (ob & cA.template ge<L, needed - 1>());
-    const uint64_t q1 = ~retreat & attc, q2 = ~retreat & ~attc;
-    const uint64_t agree = TIES ? ~maj3(anyA, anyU, anyR) : ~(anyA & anyR);
-    const uint64_t appl = ~f0;
-    const uint64_t valid = appl & ((ob & allA) | (~ob & allR));
-    const uint64_t inb = (N > 3 * (int)ME) ? ~cF.template ge<N, (int)ME + 1>() : 0ull;
-    tc.v[C_TRIALS] += (uint32_t)__popcll(val);
-    tc.v[C_AGREE] += (uint32_t)__popcll(agree & val);
-    tc.v[C_VAPPL] += (uint32_t)__popcll(appl & val);
-    tc.v[C_VALID] += (uint32_t)__popcll(valid & val);
-    tc.v[C_QR] += (uint32_t)__popcll(retreat & val);
-    tc.v[C_QA] += (uint32_t)__popcll(q1 & val);
-    tc.v[C_QU] += (uint32_t)__popcll(q2 & val);
+    const Csa<NB, T>& cXr = TIES ? cX : cA;
+    const T retreat = ~cXr.template ge<L, K0 + 1>() | (orr & ~cXr.template ge<L, K0 + 2>());
+    const T attc = cA.template ge<L, needed>() | (ob & cA.template ge<L, needed - 1>());
+    const T q1 = ~retreat & attc, q2 = ~retreat & ~attc;
+    const T agree = TIES ? ~maj3(anyA, anyU, anyR) : ~(anyA & anyR);
+    const T appl = ~f0;
+    const T valid = appl & ((ob & allA) | (~ob & allR));
+    const T inb = (N > 3 * (int)ME) ? ~cF.template ge<N, (int)ME + 1>() : (T)0;
+    tc.v[C_TRIALS] += popc_t<T>(val);
+    tc.v[C_AGREE] += popc_t<T>(agree & val);
+    tc.v[C_VAPPL] += popc_t<T>(appl & val);
+    tc.v[C_VALID] += popc_t<T>(valid & val);
+    tc.v[C_QR] += popc_t<T>(retreat & val);
+    tc.v[C_QA] += popc_t<T>(q1 & val);
+    tc.v[C_QU] += popc_t<T>(q2 & val);
     tc.v[C_UNDEF] += nU;
-    tc.v[C_INB] += (uint32_t)__popcll(inb & val);
-    tc.v[C_VIOL] += (uint32_t)__popcll(inb & (~agree | (appl & ~valid)) & val);
+    tc.v[C_INB] += popc_t<T>(inb & val);
+    tc.v[C_VIOL] += popc_t<T>(inb & (~agree | (appl & ~valid)) & val);
     tc.v[C_FTOT] += nf;
     tc.v[C_ATT] += nA;
-    inw[0] = q1;
-    inw[1] = q2;
-    inw[2] = agree;
-    inw[3] = appl;
-    inw[4] = valid;
-    inw[5] = inb;
+    out(0, q1);
+    out(1, q2);
+    out(2, agree);
+    out(3, appl);
+    out(4, valid);
+    out(5, inb);
+}
+
+// One byte of one word (trials 8k..8k+7 of the word): inw / au are the word's
+// input and root planes in LDS, k the byte.  The outcome bytes overwrite bytes
+// k of planes F[0..5] (every lane of the word reads its inputs before any lane
+// writes: all reads of a byte come from its own lane, and each lane touches
+// only its own byte k).
+template <int N, uint32_t ME>
+__device__ __forceinline__ void epilogue_byte(uint64_t* inw, const uint64_t* au, uint32_t k,
+                                              TrialCounts& tc) {
+    uint8_t* ib = reinterpret_cast<uint8_t*>(inw) + k;
+    const uint8_t* ab = reinterpret_cast<const uint8_t*>(au) + k;
+    epilogue_core<N, ME, uint32_t>([&](int p) -> uint32_t { return ib[8 * p]; },
+                                   [&](int b) -> uint32_t { return ab[8 * b]; },
+                                   [&](int o, uint32_t v) { ib[8 * o] = (uint8_t)v; }, tc);
 }
 
 template <int N, int W, uint32_t ME, int DIAG>
@@ -299,8 +403,8 @@ __device__ __forceinline__ void wave_epilogue(uint64_t* in0, const uint64_t* au0
         });
         return;
     }
-    for (uint32_t w = lane; w < (uint32_t)W; w += 64)
-        epilogue_planes<N, ME>(in0 + w * NIN, au0 + w * 2 * L, tc);
+    for (uint32_t it = lane; it < (uint32_t)W * 8; it += 64)
+        epilogue_byte<N, ME>(in0 + (it >> 3) * NIN, au0 + (it >> 3) * 2 * L, it & 7u, tc);
     __builtin_amdgcn_wave_barrier();
     const uint32_t half = lane >> 5, sh = lane & 31;
     auto bit = [&](const uint64_t* p) -> uint32_t {
@@ -553,7 +657,7 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
         const uint64_t w0 = task * W;
         const uint64_t gw0 = (first_trial >> 6) + w0;
         if constexpr (STAGED)
-            gen_words<N, W, -1>(img + G::oIN, lane, w0, seed, gs, first_trial, batch, faulty, order);
+            stage_words<N, W>(img + G::oIN, lane, w0, batch, faulty, order);
         else
             wave_inputs<N, W, DIAG>(img + G::oIN, lane, w0, seed, gs, first_trial, batch, faulty, order);
         __builtin_amdgcn_wave_barrier();
@@ -794,7 +898,7 @@ __global__ __launch_bounds__(THREADS, THREADS / 256) void k_om3q(
             uint64_t* timg = lds + t * G::task_words;
             const uint64_t w0 = (t0 + t) * W;
             if constexpr (STAGED)
-                gen_words<N, W, -1>(timg + G::tIN, lane, w0, seed, gs, first_trial, batch, faulty, order);
+                stage_words<N, W>(timg + G::tIN, lane, w0, batch, faulty, order);
             else
                 wave_inputs<N, W, 0>(timg + G::tIN, lane, w0, seed, gs, first_trial, batch, faulty, order);
             __builtin_amdgcn_wave_barrier();
