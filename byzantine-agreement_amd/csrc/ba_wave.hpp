@@ -474,6 +474,12 @@ __device__ __forceinline__ void wave_alternate_priority(uint32_t round) {
 // Every lane of the wave calls it (it holds a wave barrier); lanes with !act
 // return 0.
 // ---------------------------------------------------------------------------
+// The value of lane ^ 1 (DPP quad_perm [1,0,3,2]: a VALU move, where
+// __shfl_xor goes through ds_bpermute and waits out an LDS round trip).
+__device__ __forceinline__ uint32_t swap_pair(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+}
+
 template <int N>
 __device__ __forceinline__ uint64_t om3_round(const uint64_t* in, uint64_t l0j1, uint64_t* r2t_w,
                                               uint32_t lw, uint32_t la, bool act, uint32_t j1,
@@ -483,6 +489,16 @@ __device__ __forceinline__ uint64_t om3_round(const uint64_t* in, uint64_t l0j1,
     const uint32_t sr = j1 * C + la;             // level-1 slot (j1, j2)
     const uint32_t j2 = la + (la >= j1);
     if (act) {
+        // the round's input planes, loaded before the Philox group so their
+        // LDS latency hides under it: F[j1] (level-1 sender), F[j2] (level-2
+        // sender) and the faulty words of the block's S members
+        const uint32_t lo = j1 < j2 ? j1 : j2, hi = j1 < j2 ? j2 : j1;
+        const uint64_t fj = in[j1 + 1], fs = in[j2 + 1];
+        uint64_t Fm[S];
+        static_for<0, S>([&](auto a) {
+            const uint32_t ida = a() + (a() >= lo) + (a() + 1 >= hi);  // member a's rank
+            Fm[a()] = in[ida + 1];
+        });
         // 1. L1[j1, a] (sender j1 relays L0[j1]) and the level-2 diagonal
         //    pairs of leaf block (j1, a): one interleaved Philox group
         const uint32_t x0 = sr * S;
@@ -506,10 +522,10 @@ __device__ __forceinline__ uint64_t om3_round(const uint64_t* in, uint64_t l0j1,
             philox10_n<NPD>(pc, (uint32_t)seed, (uint32_t)(seed >> 32));
             // even lane sends its level-1 pair, odd lane its first level-2 pair
             P4 snd = odd ? pc[0] : pc[NPD - 1], rcv;
-            rcv.x = __shfl_xor(snd.x, 1, 64);
-            rcv.y = __shfl_xor(snd.y, 1, 64);
-            rcv.z = __shfl_xor(snd.z, 1, 64);
-            rcv.w = __shfl_xor(snd.w, 1, 64);
+            rcv.x = swap_pair(snd.x);
+            rcv.y = swap_pair(snd.y);
+            rcv.z = swap_pair(snd.z);
+            rcv.w = swap_pair(snd.w);
             const P4 p1 = odd ? rcv : pc[NPD - 1];
             static_for<0, NPD>([&](auto qd) {
                 const P4 q = (qd() == NPD - 1 && !odd) ? rcv : pc[qd()];
@@ -531,20 +547,15 @@ __device__ __forceinline__ uint64_t om3_round(const uint64_t* in, uint64_t l0j1,
             lie = (sr & 1u) ? ((uint64_t)pc[NPD].w << 32 | pc[NPD].z)
                             : ((uint64_t)pc[NPD].y << 32 | pc[NPD].x);
         }
-        const uint64_t fj = in[j1 + 1];
         const uint64_t par = (fj & lie) | (~fj & l0j1);
-        // 2. leaf block (j1, a): level-2 diagonal, then S(S-1) leaves
-        const uint32_t lo = j1 < j2 ? j1 : j2, hi = j1 < j2 ? j2 : j1;
-        const uint64_t fs = in[j2 + 1];  // level-2 sender: j2
+        // 2. leaf block (j1, a): level-2 diagonal (sender j2), then S(S-1) leaves
         const uint64_t oddmask = 0ull - (uint64_t)(x0 & 1u);
-        uint64_t diag[S], Fm[S], R[S];
+        uint64_t diag[S], R[S];
         static_for<0, S>([&](auto a) {
             uint64_t lie2;
             if constexpr (S % 2 == 1) lie2 = lw2[a()] ^ ((lw2[a()] ^ lw2[a() + 1]) & oddmask);
             else lie2 = lw2[a()];
             diag[a()] = (fs & lie2) | (~fs & par);
-            const uint32_t ida = a() + (a() >= lo) + (a() + 1 >= hi);  // member a's rank
-            Fm[a()] = in[ida + 1];
         });
         leaf_block<S>(ME, seed, gw, sr, diag, Fm, R);
         // receiver-major: member d of block a is receiver b = d + (d >= a)
@@ -558,8 +569,13 @@ __device__ __forceinline__ uint64_t om3_round(const uint64_t* in, uint64_t l0j1,
         // 3. R1[j1, b], b = la: L1[j1, b] (this lane's own parent) plus
         //    column b of the word's other leaf blocks a' != b
         const uint64_t* col = r2t_w + (lw * C + la) * CP;
+        uint64_t cv[C];
+        static_for<0, C>([&](auto a) { cv[a()] = col[a()]; });
+        // every column read in flight before the first add (left alone, the
+        // scheduler waited out each ds_read2 in turn)
+        __builtin_amdgcn_sched_barrier(0);
         Csa<planes_c(C)> cnt;
-        static_for<0, C>([&](auto a) { cnt.template add<a()>(col[a()]); });
+        static_for<0, C>([&](auto a) { cnt.template add<a()>(cv[a()]); });
         r1 = cnt.template ge<C, C / 2 + 1>();  // inner tie -> non-attack
     }
     __builtin_amdgcn_wave_barrier();  // r2t is rewritten by the next round

@@ -43,7 +43,7 @@ for s in $STAGES; do
          pmc_pass write WRITE_SIZE || exit $?
          pmc_pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR || exit $?
          python3 tools/pmc_summary.py gpurun_out/pmc gpurun_out/pmc_summary.json \
-           --workload "bench.py default: n=10 m=3, 1048576 trials/step" --config 10,3,1048576,auto,k_om3q > gpurun_out/pmc_summary.log 2>&1 ;;
+           --workload "bench.py default: n=10 m=3, 1048576 trials/step" --config 10,3,1048576,auto,k_om3w > gpurun_out/pmc_summary.log 2>&1 ;;
     configs) run configs 600 python -u tools/run_configs.py || exit $? ;;
     *) echo "unknown stage $s"; exit 2 ;;
   esac
