@@ -16,11 +16,14 @@ Two ways the OM(m) hot path shards:
 * Trial data-parallel (configs 2-4).  Trials are independent and every random
   draw is keyed by the GLOBAL trial index, so contiguous word-aligned trial
   ranges per rank give bit-identical results to one unsharded run.
-* One huge instance split by first-hop subtree (config 5, n=16 m=5: 4M tree
-  slots).  Rank r owns lieutenants [jb, je) as first hops; each subtree's relay
-  levels and inner majorities need only L_0[j].  Ranks exchange their level-1
-  child results (the votes every lieutenant counts about j), then every rank
-  finishes the root majorities + quorum (ba.py:159-255).
+* One huge instance split by subtree (config 5, n=16 m=5: 4M tree slots).
+  At level 1 rank r owns lieutenants [jb, je) as first hops; each subtree's
+  relay levels and inner majorities need only L_0[j].  Ranks exchange their
+  level-1 child results (the votes every lieutenant counts about j), then
+  every rank finishes the root majorities + quorum (ba.py:159-255).  At level 2
+  the units are the (n-1)(n-2) second-hop subtrees (210 at n=16: 26/27 per
+  rank over 8 ranks instead of 1-2 of 15 first hops), the exchange is their
+  level-2 results, and every rank also takes the level-1 majorities.
 """
 from __future__ import annotations
 
@@ -74,15 +77,23 @@ def run_trials_dp(comm: L.Comm, n: int, m: int, total_trials: int, *, seed: int 
     return counters
 
 
-def run_instance_split(comm: L.Comm, params: L.Params, batch: int, device: torch.device):
-    """First-hop subtree split of `batch` instances (ba_run_instance_split_multi).
-    Returns (decisions int64[batch], outcome uint8[batch], counters dict) --
-    identical on every rank and equal to an unsplit ba_run_trials."""
+def split_ranges(n: int, m: int, level: int, world: int):
+    """Unit ranges [u_begin, u_end) per rank of a split level (ba_split_share;
+    level 2 at n=16 over 8 ranks: 26/27 of 210 second-hop subtrees each)."""
+    return [L.split_share(n, m, level, world, r) for r in range(world)]
+
+
+def run_instance_split(comm: L.Comm, params: L.Params, batch: int, device: torch.device,
+                       level: int = L.SPLIT_FIRST_HOP):
+    """Subtree split of `batch` instances at `level` (1: first hop, 2: second hop;
+    ba_run_instance_split_level_multi).  Returns (decisions int64[batch], outcome
+    uint8[batch], counters dict) -- identical on every rank and equal to an
+    unsplit ba_run_trials."""
     dec = torch.empty(batch, dtype=torch.int64, device=device)
     out = torch.empty(batch, dtype=torch.uint8, device=device)
     torch.cuda.current_stream(device).synchronize()  # the comm's stream runs the job
     cnt = comm.run_instance_split(params, batch, d_decisions=dec.data_ptr(),
-                                  d_outcome=out.data_ptr())
+                                  d_outcome=out.data_ptr(), level=level)
     return dec, out, cnt
 
 
@@ -103,17 +114,21 @@ class InstanceSplitGraphs:
     """
 
     def __init__(self, device: torch.device, params: L.Params, batch: int,
-                 comm: L.Comm | None = None):
+                 comm: L.Comm | None = None, level: int = L.SPLIT_FIRST_HOP):
         self.device, self.params, self.batch, self.comm = device, params, batch, comm
+        self.level = level
         self.world = comm.nranks if comm is not None else 1
         self.rank = comm.rank if comm is not None else 0
         self.engine = L.Engine(device.index)  # own ctx: nothing else grows its scratch
-        n = params.n
-        self.jb, self.je = L.subtree_share(n, self.world, self.rank)
+        n, m = params.n, params.m
+        units = L.split_units(n, m, level)
+        if units == 0:
+            raise L.BAError(L.ENOTSUP, f"no level-{level} split for n={n}, m={m}")
+        self.jb, self.je = L.split_share(n, m, level, self.world, self.rank)
         W = (batch + 63) // 64
-        self.row = (n - 2) * W
+        self.row = (n - 1 - level) * W  # vote words per unit
         self.stream = torch.cuda.Stream(device)
-        self.votes = torch.zeros((L.vote_slots(n, params.m, 0, n - 1), W), dtype=torch.int64,
+        self.votes = torch.zeros((L.split_vote_slots(n, m, level, 0, units), W), dtype=torch.int64,
                                  device=device)
         self.dec = torch.empty(batch, dtype=torch.int64, device=device)
         self.out = torch.empty(batch, dtype=torch.uint8, device=device)
@@ -144,9 +159,10 @@ class InstanceSplitGraphs:
 
     def _tree(self):
         if self.je > self.jb:
-            self.engine.subtree_votes_device(self.params, self.batch, self.jb, self.je,
-                                             self.votes[self.jb * (self.params.n - 2):].data_ptr(),
-                                             stream=self.stream.cuda_stream)
+            per = self.params.n - 1 - self.level
+            self.engine.split_votes_device(self.params, self.batch, self.level, self.jb, self.je,
+                                           self.votes[self.jb * per:].data_ptr(),
+                                           stream=self.stream.cuda_stream)
 
     def _whole(self):
         self.cnt.zero_()
@@ -156,15 +172,17 @@ class InstanceSplitGraphs:
 
     def _gather(self):
         if self.world > 1:
-            self.comm.allgather_votes_device(self.params.n, self.params.m, self.batch,
-                                             self.votes.data_ptr(), stream=self.stream.cuda_stream)
+            self.comm.allgather_split_votes_device(self.params.n, self.params.m, self.level,
+                                                   self.batch, self.votes.data_ptr(),
+                                                   stream=self.stream.cuda_stream)
 
     def _root(self):
         self.cnt.zero_()
-        self.engine.root_from_votes_device(self.params, self.batch, self.votes.data_ptr(),
-                                           self.cnt.data_ptr(), d_decisions=self.dec.data_ptr(),
-                                           d_outcome=self.out.data_ptr(),
-                                           stream=self.stream.cuda_stream)
+        self.engine.root_from_split_votes_device(self.params, self.batch, self.level,
+                                                 self.votes.data_ptr(), self.cnt.data_ptr(),
+                                                 d_decisions=self.dec.data_ptr(),
+                                                 d_outcome=self.out.data_ptr(),
+                                                 stream=self.stream.cuda_stream)
 
     def replay(self):
         """One split call; returns (decisions, outcome, counters) (reused tensors).

@@ -28,6 +28,7 @@ ORDER_GIVEN, ORDER_RANDOM, ORDER_CONST = 0, 1, 2
 RETREAT, ATTACK, OTHER, UNDEFINED = 0, 1, 2, 2
 Q_RETREAT, Q_ATTACK, Q_UNDETERMINED = 0, 1, 2
 ENGINE_AUTO, ENGINE_FUSED, ENGINE_LEVELS = 0, 1, 2
+SPLIT_FIRST_HOP, SPLIT_SECOND_HOP = 1, 2
 COUNTER_NAMES = ["trials", "agreement", "validity_applicable", "validity", "quorum_retreat",
                  "quorum_attack", "quorum_undetermined", "undefined_decisions", "in_bound",
                  "bound_violations", "faulty_total", "attack_decisions"]
@@ -39,7 +40,9 @@ EXPORTS = ["ba_version", "ba_device_count", "ba_ctx_create", "ba_ctx_destroy", "
            "ba_ctx_device", "ba_comm_unique_id", "ba_comm_create", "ba_comm_destroy",
            "ba_trial_share", "ba_run_trials_multi", "ba_comm_rank", "ba_subtree_share",
            "ba_comm_allreduce_device", "ba_comm_allgather_votes_device",
-           "ba_run_instance_split_multi"]
+           "ba_run_instance_split_multi", "ba_split_units", "ba_split_vote_slots",
+           "ba_split_share", "ba_split_votes_device", "ba_root_from_split_votes_device",
+           "ba_comm_allgather_split_votes_device", "ba_run_instance_split_level_multi"]
 
 
 class BAError(RuntimeError):
@@ -137,6 +140,19 @@ def load(path: str | None = None):
     lib.ba_comm_allgather_votes_device.argtypes = [vp, u32, u32, u64, vp, vp]
     lib.ba_run_instance_split_multi.argtypes = [vp, vp, ctypes.POINTER(Params), u64, vp, vp, vp,
                                                 vp, ctypes.POINTER(Counters)]
+    lib.ba_split_units.argtypes = [u32, u32, u32]
+    lib.ba_split_units.restype = u64
+    lib.ba_split_vote_slots.argtypes = [u32, u32, u32, u32, u32]
+    lib.ba_split_vote_slots.restype = u64
+    lib.ba_split_share.argtypes = [u32, u32, u32, i32, i32, ctypes.POINTER(u32),
+                                   ctypes.POINTER(u32)]
+    lib.ba_split_votes_device.argtypes = [vp, ctypes.POINTER(Params), u64, u32, u32, u32, vp, vp,
+                                          vp, vp]
+    lib.ba_root_from_split_votes_device.argtypes = [vp, ctypes.POINTER(Params), u64, u32, vp, vp,
+                                                    vp, vp, vp, vp, vp]
+    lib.ba_comm_allgather_split_votes_device.argtypes = [vp, u32, u32, u32, u64, vp, vp]
+    lib.ba_run_instance_split_level_multi.argtypes = [vp, vp, ctypes.POINTER(Params), u32, u64,
+                                                      vp, vp, vp, vp, ctypes.POINTER(Counters)]
     if lib.ba_version() != ABI_VERSION:
         raise RuntimeError(f"libba_hip ABI {lib.ba_version()} != {ABI_VERSION}")
     if path is None:
@@ -269,6 +285,21 @@ class Engine:
             self.handle, ctypes.byref(params), batch, j_begin, j_end, d_faulty or None,
             d_order or None, d_votes, stream or None))
 
+    def split_votes_device(self, params: Params, batch: int, level: int, u_begin: int, u_end: int,
+                           d_votes: int, d_faulty=0, d_order=0, stream=0):
+        """Level-`level` results of split units [u_begin, u_end) (ba_split_votes_device)."""
+        _check(self.lib, self.lib.ba_split_votes_device(
+            self.handle, ctypes.byref(params), batch, level, u_begin, u_end, d_faulty or None,
+            d_order or None, d_votes, stream or None))
+
+    def root_from_split_votes_device(self, params: Params, batch: int, level: int, d_votes: int,
+                                     d_counters: int, d_faulty=0, d_order=0, d_decisions=0,
+                                     d_outcome=0, stream=0):
+        """Majorities above the split level, roots and quorum from every unit's votes."""
+        _check(self.lib, self.lib.ba_root_from_split_votes_device(
+            self.handle, ctypes.byref(params), batch, level, d_faulty or None, d_order or None,
+            d_votes, d_decisions or None, d_outcome or None, d_counters, stream or None))
+
     def root_from_votes_device(self, params: Params, batch: int, d_votes: int, d_counters: int,
                                d_faulty=0, d_order=0, d_decisions=0, d_outcome=0, stream=0):
         """Root majorities + quorum from the gathered votes of every subtree."""
@@ -298,6 +329,23 @@ def subtree_share(n: int, nranks: int, rank: int):
     lib = load()
     b, e = ctypes.c_uint32(), ctypes.c_uint32()
     _check(lib, lib.ba_subtree_share(n, nranks, rank, ctypes.byref(b), ctypes.byref(e)))
+    return b.value, e.value
+
+
+def split_units(n: int, m: int, level: int) -> int:
+    """Units of a split level (ba_split_units): n-1 first hops, (n-1)(n-2) second hops."""
+    return int(load().ba_split_units(n, m, level))
+
+
+def split_vote_slots(n: int, m: int, level: int, u_begin: int, u_end: int) -> int:
+    return int(load().ba_split_vote_slots(n, m, level, u_begin, u_end))
+
+
+def split_share(n: int, m: int, level: int, nranks: int, rank: int):
+    """[u_begin, u_end) split units of rank (ba_split_share)."""
+    lib = load()
+    b, e = ctypes.c_uint32(), ctypes.c_uint32()
+    _check(lib, lib.ba_split_share(n, m, level, nranks, rank, ctypes.byref(b), ctypes.byref(e)))
     return b.value, e.value
 
 
@@ -336,14 +384,21 @@ class Comm:
         return dict(zip(COUNTER_NAMES, [int(x) for x in cnt.v])), f.value, c.value
 
     def run_instance_split(self, params: Params, batch: int, d_decisions=0, d_outcome=0,
-                           d_faulty=0, d_order=0):
-        """First-hop split job (ba_run_instance_split_multi) -> counters dict (same on
-        every rank); decisions / outcome (batch entries) to the device buffers."""
+                           d_faulty=0, d_order=0, level: int = SPLIT_FIRST_HOP):
+        """Subtree split job (ba_run_instance_split_level_multi; level 1 = first hop,
+        2 = second hop) -> counters dict (same on every rank); decisions / outcome
+        (batch entries) to the device buffers."""
         cnt = Counters()
-        _check(self.lib, self.lib.ba_run_instance_split_multi(
-            self.engine.handle, self.handle, ctypes.byref(params), batch, d_faulty or None,
+        _check(self.lib, self.lib.ba_run_instance_split_level_multi(
+            self.engine.handle, self.handle, ctypes.byref(params), level, batch, d_faulty or None,
             d_order or None, d_decisions or None, d_outcome or None, ctypes.byref(cnt)))
         return dict(zip(COUNTER_NAMES, [int(x) for x in cnt.v]))
+
+    def allgather_split_votes_device(self, n: int, m: int, level: int, batch: int, d_votes: int,
+                                     stream=0):
+        """Every rank's split-vote rows (level 1 or 2) to every rank, in place."""
+        _check(self.lib, self.lib.ba_comm_allgather_split_votes_device(
+            self.handle, n, m, level, batch, d_votes, stream or None))
 
     def allreduce_device(self, d_counters: int, stream=0):
         """Sum the 16 device counters over the ranks in place (async on stream)."""

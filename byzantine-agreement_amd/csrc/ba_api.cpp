@@ -121,18 +121,23 @@ bool Geometry::build(uint32_t n_, uint32_t me_, uint64_t max_level_slots) {
     return true;
 }
 
-void LevelsLayout::plan(const Geometry& g, uint64_t W_, bool leaf, uint32_t jb_, uint32_t je_) {
+void LevelsLayout::plan(const Geometry& g, uint64_t W_, bool leaf, uint32_t jb_, uint32_t je_,
+                        uint32_t h_) {
     W = W_;
     jb = jb_;
     je = je_;
+    h = h_;
     leaf_fused = leaf;
     base.assign(g.me + 1, 0);
     cnt.assign(g.me + 1, 0);
     for (uint32_t k = 0; k <= g.me; ++k) {
-        if (k == 0) {
-            cnt[k] = g.S[0];
+        if (k + 1 == h && h >= 2 && je > jb) {
+            base[k] = jb;  // a second-hop tree pass: the units themselves (level-1 slots)
+            cnt[k] = je - jb;
+        } else if (k < h) {
+            cnt[k] = g.S[k];  // levels above the split (and a root pass's levels < h): whole
         } else {
-            const uint64_t q = g.S[k] / g.L;  // slots per first-hop subtree
+            const uint64_t q = g.S[k] / g.S[h - 1];  // slots per unit (a level h-1 slot)
             base[k] = (uint64_t)jb * q;
             cnt[k] = (uint64_t)(je - jb) * q;
         }
@@ -153,9 +158,10 @@ void LevelsLayout::plan(const Geometry& g, uint64_t W_, bool leaf, uint32_t jb_,
     total = o;
 }
 
-uint64_t LevelsLayout::words_per_trial_word(const Geometry& g, bool leaf, uint32_t jb, uint32_t je) {
+uint64_t LevelsLayout::words_per_trial_word(const Geometry& g, bool leaf, uint32_t jb, uint32_t je,
+                                            uint32_t h) {
     LevelsLayout l;
-    l.plan(g, 1, leaf, jb, je);
+    l.plan(g, 1, leaf, jb, je, h);
     return l.total;
 }
 }  // namespace ba
@@ -532,7 +538,7 @@ static int run_levels(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge, const LevelsJ
                       uint32_t jb, uint32_t je, bool whole, uint64_t* partials) {
     const Geometry& g = ge->g;
     const bool leaf = ctx->leaf_fusion && leaf_supported(g);
-    const uint64_t per_word = LevelsLayout::words_per_trial_word(g, leaf, jb, je) * sizeof(uint64_t);
+    const uint64_t per_word = LevelsLayout::words_per_trial_word(g, leaf, jb, je, job.h) * sizeof(uint64_t);
     uint64_t max_level = 0;
     for (uint64_t s : g.S) max_level = s > max_level ? s : max_level;
     const uint64_t words = (a.batch + 63) / 64;
@@ -545,7 +551,7 @@ static int run_levels(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge, const LevelsJ
                     (unsigned long long)words, (unsigned long long)per_word, ctx->scratch_budget,
                     whole ? ", one chunk required: split the batch" : "");
     LevelsLayout lay;
-    lay.plan(g, chunk, leaf, jb, je);
+    lay.plan(g, chunk, leaf, jb, je, job.h);
     int rc;
     if ((rc = ctx->scratch.grow(lay.total * sizeof(uint64_t))) != BA_OK) return rc;
     for (uint64_t w0 = 0; w0 < words; w0 += chunk) {
@@ -553,7 +559,7 @@ static int run_levels(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge, const LevelsJ
         const uint64_t trial0 = w0 * 64;
         const uint64_t nt = (a.batch - trial0) < wn * 64 ? (a.batch - trial0) : wn * 64;
         LevelsLayout cl;
-        cl.plan(g, wn, leaf, jb, je);
+        cl.plan(g, wn, leaf, jb, je, job.h);
         HIP_TRY(launch_levels_chunk(a, g, (const uint8_t*)ge->sender.p, (uint64_t*)ctx->scratch.p,
                                     cl, trial0, nt, partials, job));
     }
@@ -615,33 +621,55 @@ extern "C" int ba_gen_inputs_device(ba_ctx* ctx, const ba_params* p, uint64_t ba
     return BA_OK;
 }
 
+extern "C" uint64_t ba_split_units(uint32_t n, uint32_t m, uint32_t level) {
+    if (n < 3 || n > BA_MAX_GENERALS) return 0;
+    const uint32_t me = effective_depth(n, m);
+    if (level == BA_SPLIT_FIRST_HOP) return me >= 1 ? n - 1 : 0;
+    // second hop: R_2 must be a majority level, and leaf blocks (level me-2
+    // slots) must lie inside one unit
+    if (level == BA_SPLIT_SECOND_HOP) return (me >= 3 && n >= 4) ? (uint64_t)(n - 1) * (n - 2) : 0;
+    return 0;
+}
+
+extern "C" uint64_t ba_split_vote_slots(uint32_t n, uint32_t m, uint32_t level, uint32_t u_begin,
+                                        uint32_t u_end) {
+    const uint64_t units = ba_split_units(n, m, level);
+    if (units == 0 || u_begin > u_end || u_end > units) return 0;
+    return (uint64_t)(u_end - u_begin) * (n - 1 - level);  // level-h children of a level h-1 slot
+}
+
 extern "C" uint64_t ba_vote_slots(uint32_t n, uint32_t m, uint32_t j_begin, uint32_t j_end) {
-    if (n < 3 || n > BA_MAX_GENERALS || effective_depth(n, m) == 0) return 0;
-    if (j_begin > j_end || j_end > n - 1) return 0;
-    return (uint64_t)(j_end - j_begin) * (n - 2);
+    return ba_split_vote_slots(n, m, BA_SPLIT_FIRST_HOP, j_begin, j_end);
 }
 
 static int validate_split(ba_ctx* ctx, const ba_params* p, uint64_t batch, const uint32_t* d_faulty,
-                          const uint8_t* d_order) {
+                          const uint8_t* d_order, uint32_t level) {
     if (!ctx) return fail(BA_EINVAL, "ctx is NULL");
     int rc = validate(p, batch, d_faulty != nullptr, d_order != nullptr, false);
     if (rc != BA_OK) return rc;
     if (p->lie_mode != BA_LIE_PHILOX)
-        return fail(BA_ENOTSUP, "the first-hop split runs Philox lies only (table mode is OM(1))");
+        return fail(BA_ENOTSUP, "the subtree split runs Philox lies only (table mode is OM(1))");
     if (p->engine == BA_ENGINE_FUSED)
-        return fail(BA_ENOTSUP, "the first-hop split runs on the LEVELS engine");
+        return fail(BA_ENOTSUP, "the subtree split runs on the LEVELS engine");
     if (effective_depth(p->n, p->m) == 0)
         return fail(BA_ENOTSUP, "OM(0) has no relay subtrees (n=%u, m=%u)", p->n, p->m);
+    if (level != BA_SPLIT_FIRST_HOP && level != BA_SPLIT_SECOND_HOP)
+        return fail(BA_EINVAL, "split level %u (1: first hop, 2: second hop)", level);
+    if (ba_split_units(p->n, p->m, level) == 0)
+        return fail(BA_ENOTSUP, "no level-%u split for n=%u, m=%u (the second-hop split needs "
+                    "m_eff >= 3)", level, p->n, p->m);
     return BA_OK;
 }
 
-static int subtree_votes_impl(ba_ctx* ctx, const ba_params* p, uint64_t batch, uint32_t j_begin,
-                              uint32_t j_end, const uint32_t* d_faulty, const uint8_t* d_order,
-                              uint64_t* d_votes, void* stream) {
-    int rc = validate_split(ctx, p, batch, d_faulty, d_order);
+static int subtree_votes_impl(ba_ctx* ctx, const ba_params* p, uint64_t batch, uint32_t level,
+                              uint32_t j_begin, uint32_t j_end, const uint32_t* d_faulty,
+                              const uint8_t* d_order, uint64_t* d_votes, void* stream) {
+    int rc = validate_split(ctx, p, batch, d_faulty, d_order, level);
     if (rc != BA_OK) return rc;
-    if (j_begin >= j_end || j_end > p->n - 1)
-        return fail(BA_EINVAL, "subtree range [%u, %u) outside [0, %u)", j_begin, j_end, p->n - 1);
+    const uint64_t units = ba_split_units(p->n, p->m, level);
+    if (j_begin >= j_end || j_end > units)
+        return fail(BA_EINVAL, "unit range [%u, %u) outside [0, %llu)", j_begin, j_end,
+                    (unsigned long long)units);
     if (!d_votes) return fail(BA_EINVAL, "d_votes is NULL");
     if (batch == 0) return BA_OK;
     HIP_TRY(hipSetDevice(ctx->device));
@@ -652,15 +680,16 @@ static int subtree_votes_impl(ba_ctx* ctx, const ba_params* p, uint64_t batch, u
     a.members = (const uint64_t*)ge->members.p;
     LevelsJob job;
     job.root = false;
+    job.h = level;
     job.votes_out = d_votes;
     return run_levels(ctx, a, ge, job, j_begin, j_end, true, nullptr);
 }
 
-static int root_from_votes_impl(ba_ctx* ctx, const ba_params* p, uint64_t batch,
+static int root_from_votes_impl(ba_ctx* ctx, const ba_params* p, uint64_t batch, uint32_t level,
                                 const uint32_t* d_faulty, const uint8_t* d_order,
                                 const uint64_t* d_votes, uint64_t* d_decisions, uint8_t* d_outcome,
                                 uint64_t* d_counters, void* stream) {
-    int rc = validate_split(ctx, p, batch, d_faulty, d_order);
+    int rc = validate_split(ctx, p, batch, d_faulty, d_order, level);
     if (rc != BA_OK) return rc;
     if (!d_votes || !d_counters) return fail(BA_EINVAL, "d_votes and d_counters are required");
     if (batch == 0) return BA_OK;
@@ -673,8 +702,9 @@ static int root_from_votes_impl(ba_ctx* ctx, const ba_params* p, uint64_t batch,
     a.members = (const uint64_t*)ge->members.p;
     LevelsJob job;
     job.tree = false;
+    job.h = level;
     job.votes_in = d_votes;
-    // an empty subtree range: only the inputs and L_0 are materialised
+    // an empty unit range: only the inputs and levels 0..h-1 are materialised
     return run_levels(ctx, a, ge, job, 0, 0, true, (uint64_t*)ctx->partials.p);
 }
 
@@ -702,23 +732,40 @@ extern "C" int ba_run_trials_device(ba_ctx* ctx, const ba_params* p, uint64_t ba
     });
 }
 
+extern "C" int ba_split_votes_device(ba_ctx* ctx, const ba_params* p, uint64_t batch,
+                                     uint32_t level, uint32_t u_begin, uint32_t u_end,
+                                     const uint32_t* d_faulty, const uint8_t* d_order,
+                                     uint64_t* d_votes, void* stream) {
+    return ordered(ctx, stream, [&] {
+        return subtree_votes_impl(ctx, p, batch, level, u_begin, u_end, d_faulty, d_order, d_votes,
+                                  stream);
+    });
+}
+
+extern "C" int ba_root_from_split_votes_device(ba_ctx* ctx, const ba_params* p, uint64_t batch,
+                                               uint32_t level, const uint32_t* d_faulty,
+                                               const uint8_t* d_order, const uint64_t* d_votes,
+                                               uint64_t* d_decisions, uint8_t* d_outcome,
+                                               uint64_t* d_counters, void* stream) {
+    return ordered(ctx, stream, [&] {
+        return root_from_votes_impl(ctx, p, batch, level, d_faulty, d_order, d_votes, d_decisions,
+                                    d_outcome, d_counters, stream);
+    });
+}
+
 extern "C" int ba_subtree_votes_device(ba_ctx* ctx, const ba_params* p, uint64_t batch,
                                        uint32_t j_begin, uint32_t j_end, const uint32_t* d_faulty,
                                        const uint8_t* d_order, uint64_t* d_votes, void* stream) {
-    return ordered(ctx, stream, [&] {
-        return subtree_votes_impl(ctx, p, batch, j_begin, j_end, d_faulty, d_order, d_votes,
-                                  stream);
-    });
+    return ba_split_votes_device(ctx, p, batch, BA_SPLIT_FIRST_HOP, j_begin, j_end, d_faulty,
+                                 d_order, d_votes, stream);
 }
 
 extern "C" int ba_root_from_votes_device(ba_ctx* ctx, const ba_params* p, uint64_t batch,
                                          const uint32_t* d_faulty, const uint8_t* d_order,
                                          const uint64_t* d_votes, uint64_t* d_decisions,
                                          uint8_t* d_outcome, uint64_t* d_counters, void* stream) {
-    return ordered(ctx, stream, [&] {
-        return root_from_votes_impl(ctx, p, batch, d_faulty, d_order, d_votes, d_decisions,
-                                    d_outcome, d_counters, stream);
-    });
+    return ba_root_from_split_votes_device(ctx, p, batch, BA_SPLIT_FIRST_HOP, d_faulty, d_order,
+                                           d_votes, d_decisions, d_outcome, d_counters, stream);
 }
 
 // ---------------------------------------------------------------------------

@@ -101,6 +101,48 @@ __host__ __device__ __forceinline__ void philox_mul2(uint32_t x, uint32_t z, uin
     p1 = (uint64_t)0xCD9E8D57u * z;
 }
 
+// Both products of round I for G interleaved calls (philox10_n).  From round 2
+// on, G = 2..4 calls' 2G products go into ONE asm statement: the hazard
+// recognizer treats every inline-asm def as a possible dst-forwarding hazard
+// and puts an s_nop between an asm and the next instruction that reads or
+// writes any of its defs -- including the next asm's carry-out SGPR -- so one
+// statement per group instead of one per call removes most of those nops.
+template <int I, int G>
+__host__ __device__ __forceinline__ void philox_mul2_n(const P4 (&c)[G], uint64_t (&p0)[G],
+                                                       uint64_t (&p1)[G]) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(BA_PHILOX_C) && !defined(BA_MAD_SPLIT_ASM)
+    if constexpr (I >= 2 && G >= 2 && G <= 4) {
+        uint64_t cc;
+        constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+        if constexpr (G == 2)
+            asm("v_mad_u64_u32 %0, %4, %5, %9, 0\n\tv_mad_u64_u32 %1, %4, %6, %10, 0\n\t"
+                "v_mad_u64_u32 %2, %4, %7, %9, 0\n\tv_mad_u64_u32 %3, %4, %8, %10, 0"
+                : "=&v"(p0[0]), "=&v"(p1[0]), "=&v"(p0[1]), "=&v"(p1[1]), "=&s"(cc)
+                : "v"(c[0].x), "v"(c[0].z), "v"(c[1].x), "v"(c[1].z), "s"(M0), "s"(M1));
+        else if constexpr (G == 3)
+            asm("v_mad_u64_u32 %0, %6, %7, %13, 0\n\tv_mad_u64_u32 %1, %6, %8, %14, 0\n\t"
+                "v_mad_u64_u32 %2, %6, %9, %13, 0\n\tv_mad_u64_u32 %3, %6, %10, %14, 0\n\t"
+                "v_mad_u64_u32 %4, %6, %11, %13, 0\n\tv_mad_u64_u32 %5, %6, %12, %14, 0"
+                : "=&v"(p0[0]), "=&v"(p1[0]), "=&v"(p0[1]), "=&v"(p1[1]), "=&v"(p0[2]),
+                  "=&v"(p1[2]), "=&s"(cc)
+                : "v"(c[0].x), "v"(c[0].z), "v"(c[1].x), "v"(c[1].z), "v"(c[2].x), "v"(c[2].z),
+                  "s"(M0), "s"(M1));
+        else
+            asm("v_mad_u64_u32 %0, %8, %9, %17, 0\n\tv_mad_u64_u32 %1, %8, %10, %18, 0\n\t"
+                "v_mad_u64_u32 %2, %8, %11, %17, 0\n\tv_mad_u64_u32 %3, %8, %12, %18, 0\n\t"
+                "v_mad_u64_u32 %4, %8, %13, %17, 0\n\tv_mad_u64_u32 %5, %8, %14, %18, 0\n\t"
+                "v_mad_u64_u32 %6, %8, %15, %17, 0\n\tv_mad_u64_u32 %7, %8, %16, %18, 0"
+                : "=&v"(p0[0]), "=&v"(p1[0]), "=&v"(p0[1]), "=&v"(p1[1]), "=&v"(p0[2]),
+                  "=&v"(p1[2]), "=&v"(p0[3]), "=&v"(p1[3]), "=&s"(cc)
+                : "v"(c[0].x), "v"(c[0].z), "v"(c[1].x), "v"(c[1].z), "v"(c[2].x), "v"(c[2].z),
+                  "v"(c[3].x), "v"(c[3].z), "s"(M0), "s"(M1));
+        return;
+    }
+#endif
+#pragma unroll
+    for (int g = 0; g < G; ++g) philox_mul2<I>(c[g].x, c[g].z, p0[g], p1[g]);
+}
+
 __host__ __device__ __forceinline__ P4 philox10(P4 c, uint32_t k0, uint32_t k1) {
     static_for_h<0, 10>([&](auto i) {
         uint64_t p0, p1;
@@ -125,8 +167,7 @@ template <int G>
 __host__ __device__ __forceinline__ void philox10_n(P4 (&c)[G], uint32_t k0, uint32_t k1) {
     static_for_h<0, 10>([&](auto i) {
         uint64_t p0[G], p1[G];
-#pragma unroll
-        for (int g = 0; g < G; ++g) philox_mul2<i()>(c[g].x, c[g].z, p0[g], p1[g]);
+        philox_mul2_n<i(), G>(c, p0, p1);
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             P4 n;

@@ -81,24 +81,31 @@ struct Geometry {
 // base[k] = jb * S[k] / L; level 0 (L slots) is always whole.
 struct LevelsLayout {
     uint64_t W = 0;
-    uint32_t jb = 0, je = 0;
+    // split units [jb, je) at level h-1: first-hop lieutenants (h = 1) or
+    // level-1 slots, i.e. second-hop subtrees (h = 2).  Levels < h are whole,
+    // except a second-hop tree pass's unit level (level 1: the range only).
+    uint32_t jb = 0, je = 0, h = 1;
     uint64_t F = 0, OB = 0, OO = 0, VAL = 0;
     std::vector<uint64_t> Lk, Rp;  // Rp[p] valid for 1 <= p < me
     std::vector<uint64_t> base, cnt;
     uint64_t total = 0;
     bool leaf_fused = false;       // L_{me-1}, L_me not materialised (k_leaf)
-    void plan(const Geometry& g, uint64_t W, bool leaf, uint32_t jb, uint32_t je);
-    static uint64_t words_per_trial_word(const Geometry& g, bool leaf, uint32_t jb, uint32_t je);
+    void plan(const Geometry& g, uint64_t W, bool leaf, uint32_t jb, uint32_t je, uint32_t h = 1);
+    static uint64_t words_per_trial_word(const Geometry& g, bool leaf, uint32_t jb, uint32_t je,
+                                         uint32_t h = 1);
 };
 
-// What one LEVELS pass computes.  The default is a whole trial batch.  The
-// first-hop split runs `tree` on a subtree range and leaves its level-1 child
-// results (R_1, or L_1 at depth 1) in votes_out; `root` alone reads the
-// gathered votes of every subtree (votes_in) for the root majorities.
+// What one LEVELS pass computes.  The default is a whole trial batch.  A
+// split at level h runs `tree` on a unit range (first-hop subtrees for h = 1,
+// second-hop subtrees for h = 2) and leaves the units' level-h results (R_h,
+// or L_1 at depth 1) in votes_out; `root` alone reads the gathered votes of
+// every unit (votes_in), relays levels 0..h-1 itself, takes the majorities of
+// levels h-1..1 and the root majorities + quorum.
 struct LevelsJob {
     bool tree = true, root = true;
-    uint64_t* votes_out = nullptr;       // [ (je-jb)(L-1) slots ][ W ]
-    const uint64_t* votes_in = nullptr;  // [ L(L-1) slots ][ W ]
+    uint32_t h = 1;                      // split level (1: first hop, 2: second hop)
+    uint64_t* votes_out = nullptr;       // [ units' level-h slots ][ W ]
+    const uint64_t* votes_in = nullptr;  // [ all level-h slots ][ W ]
 };
 
 constexpr int kPartialRows = 2048;  // max epilogue blocks per launch

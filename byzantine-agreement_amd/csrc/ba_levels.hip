@@ -660,17 +660,17 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
     // where level k / majority p live: scratch, except the level-1 child
     // results (R_1, or L_1 at depth 1) that a subtree pass leaves in votes_out
     auto Lptr = [&](uint32_t k) -> uint64_t* {
-        if (k == 1 && g.me == 1 && job.votes_out) return job.votes_out;
+        if (k == 1 && g.me == 1 && job.h == 1 && job.votes_out) return job.votes_out;
         return scratch + lay.Lk[k];
     };
     auto Rptr = [&](uint32_t p) -> uint64_t* {
-        if (p == 1 && job.votes_out) return job.votes_out;
+        if (p == job.h && job.votes_out) return job.votes_out;
         return scratch + lay.Rp[p];
     };
     // relay, top-down (levels 0..me, or 0..me-2 when the two bottom levels
     // are fused into the leaf-block kernel and never materialised).  Level 0
     // is always whole; a root-only pass stops there.
-    const uint32_t ktop = !job.tree ? 0 : (lay.leaf_fused ? g.me - 2 : g.me);
+    const uint32_t ktop = !job.tree ? job.h - 1 : (lay.leaf_fused ? g.me - 2 : g.me);
     // levels 0..kf in one k_relay_top launch; a materialised leaf level (no
     // leaf fusion) stays a k_relay launch, since a chain walk per leaf pair
     // would multiply the biggest level's draws.  BA_NO_TOP_RELAY=1: one
@@ -727,7 +727,9 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
     // block's S column results, so R_{me-1} is never stored and the inner
     // majority launches start one level higher.  BA_NO_LEAF_UP=1: off (A/B).
     const bool no_up = getenv("BA_NO_LEAF_UP") && atoi(getenv("BA_NO_LEAF_UP")) != 0;
-    const bool leaf_up = job.tree && lay.leaf_fused && g.me >= 3 && !no_up;
+    // (a split's tree pass keeps its vote level: leaf-up only below it)
+    const bool leaf_up = job.tree && lay.leaf_fused && g.me >= 3 && !no_up &&
+                         g.me - 2 >= (job.votes_out ? job.h : 1u);
     if (job.tree && lay.leaf_fused) {  // L_{me-1} and L_me on the fly: R_{me-1} from L_{me-2}
         // leaf blocks = slots of level me-2; level 0 is stored whole, but its
         // subtree range is the first-hop lieutenants [jb, je) themselves
@@ -740,13 +742,17 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
         if (e != hipSuccess) return e;
     }
     // inner majorities, bottom-up: levels me-1..1 (no leaf fusion), me-2..1
-    // (k_leaf wrote R_{me-1}) or me-3..1 (k_leaf wrote R_{me-2})
-    const int pdeep = job.tree ? (int)g.me - (lay.leaf_fused ? (leaf_up ? 3 : 2) : 1) : 0;
-    for (int p = pdeep; p >= 1; --p) {
+    // (k_leaf wrote R_{me-1}) or me-3..1 (k_leaf wrote R_{me-2}); a split's
+    // tree pass stops at its vote level h, its root pass takes levels h-1..1
+    // over the gathered votes
+    const int pdeep = job.tree ? (int)g.me - (lay.leaf_fused ? (leaf_up ? 3 : 2) : 1) : (int)job.h - 1;
+    const int plow = (job.tree && job.votes_out) ? (int)job.h : 1;
+    for (int p = pdeep; p >= plow; --p) {
         const uint32_t s = g.L - (uint32_t)p;
         const uint32_t work = (uint32_t)(lay.cnt[p] * W);
         const uint32_t ybase = (uint32_t)lay.base[p], cbase = (uint32_t)lay.base[p + 1];
-        const uint64_t* C = (p + 1 == (int)g.me) ? Lptr(p + 1) : Rptr(p + 1);
+        const uint64_t* C = (!job.tree && p + 1 == (int)job.h) ? job.votes_in
+                            : (p + 1 == (int)g.me) ? Lptr(p + 1) : Rptr(p + 1);
         const uint64_t* Lp = Lptr(p);
         uint64_t* Rp = Rptr(p);
         ProfScope ps(a.prof, p + 1 == (int)g.me ? "k_majority_leaf" : "k_majority_inner", st);
@@ -761,7 +767,7 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
     }
     if (!job.root) return hipSuccess;
     // root + quorum epilogue over L_0 and the level-1 child results
-    const uint64_t* C1 = job.votes_in ? job.votes_in
+    const uint64_t* C1 = (job.votes_in && job.h == 1) ? job.votes_in
                          : (g.me >= 2 ? scratch + lay.Rp[1] : (g.me == 1 ? scratch + lay.Lk[1] : nullptr));
     const uint32_t blocks = blocks_for(W * 64, kPartialRows);
     uint64_t* dec = a.decisions ? a.decisions + trial0 : nullptr;

@@ -195,6 +195,17 @@ extern "C" int ba_subtree_share(uint32_t n, int nranks, int rank, uint32_t* j_be
     return BA_OK;
 }
 
+extern "C" int ba_split_share(uint32_t n, uint32_t m, uint32_t level, int nranks, int rank,
+                              uint32_t* u_begin, uint32_t* u_end) {
+    const uint64_t U = ba_split_units(n, m, level);
+    if (U == 0 || nranks < 1 || rank < 0 || rank >= nranks || !u_begin || !u_end)
+        return failf(BA_EINVAL, "level-%u split of n=%u, m=%u, rank %d of %d ranks", level, n, m,
+                     rank, nranks);
+    *u_begin = (uint32_t)(U * (uint64_t)rank / (uint64_t)nranks);
+    *u_end = (uint32_t)(U * (uint64_t)(rank + 1) / (uint64_t)nranks);
+    return BA_OK;
+}
+
 // ---------------------------------------------------------------------------
 // collectives (asynchronous on `stream`)
 // ---------------------------------------------------------------------------
@@ -208,21 +219,22 @@ extern "C" int ba_comm_allreduce_device(struct ba_comm* comm, uint64_t* d_counte
     return BA_OK;
 }
 
-extern "C" int ba_comm_allgather_votes_device(struct ba_comm* comm, uint32_t n, uint32_t m,
-                                              uint64_t batch, uint64_t* d_votes, void* stream) {
+extern "C" int ba_comm_allgather_split_votes_device(struct ba_comm* comm, uint32_t n, uint32_t m,
+                                                    uint32_t level, uint64_t batch,
+                                                    uint64_t* d_votes, void* stream) {
     if (!comm || !d_votes) return failf(BA_EINVAL, "comm and d_votes are required");
-    if (ba_vote_slots(n, m, 0, n >= 2 ? n - 1 : 0) == 0)
-        return failf(BA_EINVAL, "no first-hop votes for n=%u, m=%u", n, m);
+    const uint64_t units = ba_split_units(n, m, level);
+    if (units == 0) return failf(BA_EINVAL, "no level-%u split votes for n=%u, m=%u", level, n, m);
     if (hipSetDevice(comm->device) != hipSuccess) return failf(BA_EDEVICE, "hipSetDevice");
-    const uint64_t W = (batch + 63) / 64, row = (uint64_t)(n - 2) * W;
+    const uint64_t W = (batch + 63) / 64, row = (uint64_t)(n - 1 - level) * W;  // words per unit
     Rccl& r = rccl();
     ncclResult_t e = r.group_start();
     for (int q = 0; q < comm->nranks && e == ncclSuccess; ++q) {
-        uint32_t jb = 0, je = 0;
-        (void)ba_subtree_share(n, comm->nranks, q, &jb, &je);
-        if (je == jb) continue;
-        uint64_t* part = d_votes + (uint64_t)jb * row;  // rank q's rows, in place on every rank
-        e = r.broadcast(part, part, (size_t)(je - jb) * row, ncclUint64, q, comm->comm,
+        uint32_t ub = 0, ue = 0;
+        (void)ba_split_share(n, m, level, comm->nranks, q, &ub, &ue);
+        if (ue == ub) continue;
+        uint64_t* part = d_votes + (uint64_t)ub * row;  // rank q's rows, in place on every rank
+        e = r.broadcast(part, part, (size_t)(ue - ub) * row, ncclUint64, q, comm->comm,
                         (hipStream_t)stream);
     }
     const ncclResult_t e2 = r.group_end();
@@ -230,6 +242,12 @@ extern "C" int ba_comm_allgather_votes_device(struct ba_comm* comm, uint32_t n, 
         return failf(BA_EDEVICE, "vote all-gather (grouped ncclBroadcast): %s",
                      r.error_string(e != ncclSuccess ? e : e2));
     return BA_OK;
+}
+
+extern "C" int ba_comm_allgather_votes_device(struct ba_comm* comm, uint32_t n, uint32_t m,
+                                              uint64_t batch, uint64_t* d_votes, void* stream) {
+    return ba_comm_allgather_split_votes_device(comm, n, m, BA_SPLIT_FIRST_HOP, batch, d_votes,
+                                                stream);
 }
 
 // ---------------------------------------------------------------------------
@@ -302,20 +320,24 @@ extern "C" int ba_run_trials_multi(struct ba_ctx* ctx, struct ba_comm* comm, con
     return finish_job(comm, local, counters_out, true);
 }
 
-extern "C" int ba_run_instance_split_multi(struct ba_ctx* ctx, struct ba_comm* comm,
-                                           const ba_params* p, uint64_t batch,
-                                           const uint32_t* d_faulty_mask, const uint8_t* d_order,
-                                           uint64_t* d_decisions, uint8_t* d_outcome,
-                                           ba_counters* counters_out) {
+extern "C" int ba_run_instance_split_level_multi(struct ba_ctx* ctx, struct ba_comm* comm,
+                                                 const ba_params* p, uint32_t level,
+                                                 uint64_t batch, const uint32_t* d_faulty_mask,
+                                                 const uint8_t* d_order, uint64_t* d_decisions,
+                                                 uint8_t* d_outcome, ba_counters* counters_out) {
     if (!ctx || !comm || !p) return failf(BA_EINVAL, "ctx, comm and params are required");
     int rc = begin_job(comm);
     if (rc != BA_OK) return rc;
     int local = ba_validate_internal(p, batch);
     const uint32_t n = p->n;
-    const uint64_t slots = local == BA_OK ? ba_vote_slots(n, p->m, 0, n - 1) : 0;
+    const uint64_t units = local == BA_OK ? ba_split_units(n, p->m, level) : 0;
+    const uint64_t slots = local == BA_OK ? ba_split_vote_slots(n, p->m, level, 0, (uint32_t)units) : 0;
     if (local == BA_OK && slots == 0)
-        local = failf(BA_ENOTSUP, "OM(0) has no relay subtrees (n=%u, m=%u)", n, p->m);
-    if (comm->nranks == 1) {  // one rank owns every subtree: the unsplit pass, no vote array
+        local = (level == BA_SPLIT_FIRST_HOP || level == BA_SPLIT_SECOND_HOP)
+                    ? failf(BA_ENOTSUP, "no level-%u split for n=%u, m=%u (OM(0) has no relay "
+                            "subtrees; the second-hop split needs m_eff >= 3)", level, n, p->m)
+                    : failf(BA_EINVAL, "split level %u (1: first hop, 2: second hop)", level);
+    if (comm->nranks == 1) {  // one rank owns every unit: the unsplit pass, no vote array
         if (local == BA_OK && batch > 0)
             local = ba_run_trials_device(ctx, p, batch, d_faulty_mask, d_order, nullptr, nullptr,
                                          d_decisions, d_outcome, comm->d_cnt, comm->stream);
@@ -334,20 +356,31 @@ extern "C" int ba_run_instance_split_multi(struct ba_ctx* ctx, struct ba_comm* c
             comm->votes_bytes = need;
     }
     if (local == BA_OK && batch > 0) {
-        uint32_t jb = 0, je = 0;
-        (void)ba_subtree_share(n, comm->nranks, comm->rank, &jb, &je);
-        if (je > jb)
-            local = ba_subtree_votes_device(ctx, p, batch, jb, je, d_faulty_mask, d_order,
-                                            comm->d_votes + (uint64_t)jb * (n - 2) * W,
-                                            comm->stream);
+        uint32_t ub = 0, ue = 0;
+        (void)ba_split_share(n, p->m, level, comm->nranks, comm->rank, &ub, &ue);
+        if (ue > ub)
+            local = ba_split_votes_device(ctx, p, batch, level, ub, ue, d_faulty_mask, d_order,
+                                          comm->d_votes + (uint64_t)ub * (n - 1 - level) * W,
+                                          comm->stream);
     }
     // the exchange runs whatever happened locally (no rank may skip a collective)
     if (slots > 0 && batch > 0) {
-        const int e = ba_comm_allgather_votes_device(comm, n, p->m, batch, comm->d_votes, comm->stream);
+        const int e = ba_comm_allgather_split_votes_device(comm, n, p->m, level, batch,
+                                                           comm->d_votes, comm->stream);
         if (local == BA_OK) local = e;
     }
     if (local == BA_OK && batch > 0)
-        local = ba_root_from_votes_device(ctx, p, batch, d_faulty_mask, d_order, comm->d_votes,
-                                          d_decisions, d_outcome, comm->d_cnt, comm->stream);
+        local = ba_root_from_split_votes_device(ctx, p, batch, level, d_faulty_mask, d_order,
+                                                comm->d_votes, d_decisions, d_outcome, comm->d_cnt,
+                                                comm->stream);
     return finish_job(comm, local, counters_out, false);
+}
+
+extern "C" int ba_run_instance_split_multi(struct ba_ctx* ctx, struct ba_comm* comm,
+                                           const ba_params* p, uint64_t batch,
+                                           const uint32_t* d_faulty_mask, const uint8_t* d_order,
+                                           uint64_t* d_decisions, uint8_t* d_outcome,
+                                           ba_counters* counters_out) {
+    return ba_run_instance_split_level_multi(ctx, comm, p, BA_SPLIT_FIRST_HOP, batch, d_faulty_mask,
+                                             d_order, d_decisions, d_outcome, counters_out);
 }

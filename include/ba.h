@@ -205,6 +205,41 @@ int ba_root_from_votes_device(struct ba_ctx* ctx, const ba_params* p, uint64_t b
                               const uint64_t* d_votes, uint64_t* d_decisions, uint8_t* d_outcome,
                               uint64_t* d_counters, void* stream);
 
+/* ---- the same split at either of two levels ------------------------------
+ * level 1 (BA_SPLIT_FIRST_HOP): units = the n-1 first-hop subtrees; exactly
+ *   the entries above (votes R_1 / L_1, n-2 per unit).
+ * level 2 (BA_SPLIT_SECOND_HOP): units = the (n-1)(n-2) second-hop subtrees,
+ *   one per level-1 slot (j, a) in path order u = j(n-2) + k, a = k + (k >= j);
+ *   a unit's relay levels >= 2 and majorities >= 2 need only L_1[j.a], so a
+ *   rank owning units [u_begin, u_end) computes their level-2 results
+ *   R_2[j.a.r] (n-3 per unit, receivers r in rank order) into
+ *       d_votes[(u - u_begin)(n-3) + c][w].
+ *   The root pass relays levels 0 and 1 itself (cheap: (n-1)^2 slots), takes
+ *   the level-1 majorities over the gathered R_2 and finishes as above.  Needs
+ *   m_eff >= 3.  15 first hops split 1,2,..,2 over 8 ranks (slowest rank 2/15
+ *   of the tree); 210 second hops split 26/27 (27/210).
+ * ba_split_units: the units of a level (0 if the level does not apply);
+ * ba_split_vote_slots: vote rows of units [u_begin, u_end);
+ * ba_split_share: rank's contiguous unit range, units split as evenly as
+ * possible (ranks beyond the unit count get empty ranges).  The level-1 forms
+ * equal ba_vote_slots / ba_subtree_share / ba_subtree_votes_device /
+ * ba_root_from_votes_device. */
+#define BA_SPLIT_FIRST_HOP 1
+#define BA_SPLIT_SECOND_HOP 2
+uint64_t ba_split_units(uint32_t n, uint32_t m, uint32_t level);
+uint64_t ba_split_vote_slots(uint32_t n, uint32_t m, uint32_t level, uint32_t u_begin,
+                             uint32_t u_end);
+int ba_split_share(uint32_t n, uint32_t m, uint32_t level, int nranks, int rank,
+                   uint32_t* u_begin, uint32_t* u_end);
+int ba_split_votes_device(struct ba_ctx* ctx, const ba_params* p, uint64_t batch, uint32_t level,
+                          uint32_t u_begin, uint32_t u_end, const uint32_t* d_faulty_mask,
+                          const uint8_t* d_order, uint64_t* d_votes, void* stream);
+int ba_root_from_split_votes_device(struct ba_ctx* ctx, const ba_params* p, uint64_t batch,
+                                    uint32_t level, const uint32_t* d_faulty_mask,
+                                    const uint8_t* d_order, const uint64_t* d_votes,
+                                    uint64_t* d_decisions, uint8_t* d_outcome,
+                                    uint64_t* d_counters, void* stream);
+
 /* ---- multi-GPU (no ba.py analogue: its generals are threads of
  * one process, ba.py:104-112) ----------------------------------------------
  * One process per GPU.  Rank 0 calls ba_comm_unique_id and ships the
@@ -244,6 +279,11 @@ int ba_subtree_share(uint32_t n, int nranks, int rank, uint32_t* j_begin, uint32
 int ba_comm_allreduce_device(struct ba_comm* comm, uint64_t* d_counters, void* stream);
 int ba_comm_allgather_votes_device(struct ba_comm* comm, uint32_t n, uint32_t m, uint64_t batch,
                                    uint64_t* d_votes, void* stream);
+/* the same all-gather for a split at `level` (d_votes: the full
+ * [ba_split_vote_slots(n, m, level, 0, units)][W] array) */
+int ba_comm_allgather_split_votes_device(struct ba_comm* comm, uint32_t n, uint32_t m,
+                                         uint32_t level, uint64_t batch, uint64_t* d_votes,
+                                         void* stream);
 
 /* Whole jobs, blocking (they return after the collectives, on the comm's
  * stream).  A rank whose local work fails still joins every collective and
@@ -269,6 +309,13 @@ int ba_run_instance_split_multi(struct ba_ctx* ctx, struct ba_comm* comm, const 
                                 uint64_t batch, const uint32_t* d_faulty_mask,
                                 const uint8_t* d_order, uint64_t* d_decisions,
                                 uint8_t* d_outcome, ba_counters* counters_out);
+/* ba_run_instance_split_multi at a split level (1 = the call above, 2 =
+ * second-hop units, m_eff >= 3) */
+int ba_run_instance_split_level_multi(struct ba_ctx* ctx, struct ba_comm* comm,
+                                      const ba_params* p, uint32_t level, uint64_t batch,
+                                      const uint32_t* d_faulty_mask, const uint8_t* d_order,
+                                      uint64_t* d_decisions, uint8_t* d_outcome,
+                                      ba_counters* counters_out);
 
 /* Per-kernel timing (tracing aux subsystem; replaces nothing in ba.py, which
  * only prints).  When enabled, every kernel the ctx launches is bracketed by

@@ -363,3 +363,54 @@ int ba_oracle_votes(uint32_t n, uint32_t m, uint64_t seed, uint32_t faulty_mode,
     }
     return 0;
 }
+
+/* Level-2 results of the second-hop split: for every level-1
+ * slot (j, a) -- unit u = j*(L-1) + k with a = k + (k >= j) -- and every
+ * receiver r not in {j, a}, child c in rank order, R_2[j.a.r] = the value r
+ * attributes to path j.a after the recursive majority below it (ba.py:159-195
+ * generalised).  votes[((i*L*(L-1) + u)*(L-2) + c].  Needs m_eff >= 3 (R_2 is
+ * a majority level) and n >= 4. */
+int ba_oracle_votes2(uint32_t n, uint32_t m, uint64_t seed, uint32_t faulty_mode, uint32_t f,
+                     uint32_t order_mode, uint32_t order_value, uint64_t first_trial,
+                     uint64_t batch, const uint32_t* faulty, const uint8_t* order, uint8_t* votes,
+                     int threads) {
+    if (n < 4 || n > MAXN || m > MAXM) return E_INVAL;
+    if (faulty_mode == FAULTY_GIVEN && !faulty) return E_INVAL;
+    if (order_mode == ORDER_GIVEN && !order) return E_INVAL;
+    if (first_trial & 63) return E_INVAL;
+    const int L = (int)n - 1;
+    const int me = (int)m < (int)n - 2 ? (int)m : (int)n - 2;
+    if (me < 3) return E_NOTSUP;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#else
+    (void)threads;
+#endif
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t i = 0; i < (int64_t)batch; ++i) {
+        uint64_t t = first_trial + (uint64_t)i;
+        uint32_t fmask = faulty_mode == FAULTY_GIVEN ? faulty[i] : 0;
+        uint8_t oc = order_mode == ORDER_GIVEN ? order[i] : 0;
+        ba_oracle_gen(n, seed, faulty_mode, f, order_mode, order_value, t,
+                      faulty_mode == FAULTY_GIVEN ? NULL : &fmask,
+                      order_mode == ORDER_GIVEN ? NULL : &oc);
+        fmask &= (n >= 32) ? 0xFFFFFFFFu : ((1u << n) - 1u);
+        tctx c = {seed, t, L, me, fmask, oc == V_ATTACK};
+        int path[MAXM + 2];
+        for (int j = 0; j < L; ++j)
+            for (int k = 0; k < L - 1; ++k) {
+                const int a = k + (k >= j);
+                const uint64_t u = (uint64_t)j * (L - 1) + k;
+                int ch = 0;
+                for (int r = 0; r < L; ++r) {
+                    if (r == j || r == a) continue;
+                    path[0] = j;
+                    path[1] = a;
+                    votes[((uint64_t)i * L * (L - 1) + u) * (L - 2) + ch] =
+                        (uint8_t)om_resolve(&c, path, 2, r, (1u << j) | (1u << a));
+                    ++ch;
+                }
+            }
+    }
+    return 0;
+}

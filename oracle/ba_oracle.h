@@ -51,6 +51,11 @@ int ba_oracle_votes(uint32_t n, uint32_t m, uint64_t seed, uint32_t faulty_mode,
                     uint32_t order_mode, uint32_t order_value, uint64_t first_trial,
                     uint64_t batch, const uint32_t* faulty, const uint8_t* order, uint8_t* votes,
                     int threads);
+/* Level-2 results R_2 of every level-1 slot (second-hop split), uint8[batch][L(L-1)][L-2]. */
+int ba_oracle_votes2(uint32_t n, uint32_t m, uint64_t seed, uint32_t faulty_mode, uint32_t f,
+                    uint32_t order_mode, uint32_t order_value, uint64_t first_trial,
+                    uint64_t batch, const uint32_t* faulty, const uint8_t* order, uint8_t* votes,
+                    int threads);
 
 #ifdef __cplusplus
 }

@@ -32,6 +32,7 @@ def load():
         lib.ba_oracle_gen.argtypes = [u32, u64, u32, u32, u32, u32, u64, vp, vp]
         lib.ba_oracle_votes.argtypes = [u32, u32, u64, u32, u32, u32, u32, u64, u64, vp, vp, vp,
                                         ctypes.c_int]
+        lib.ba_oracle_votes2.argtypes = lib.ba_oracle_votes.argtypes
         lib.ba_sliced_run.argtypes = [u32, u32, u64, u32, u32, u32, u32, u64, u64, vp, vp, vp, vp,
                                       vp, ctypes.c_int]
         lib.ba_sliced_gen.argtypes = [u32, u64, u32, u32, u32, u32, u64, u64, vp, vp, ctypes.c_int]
@@ -79,8 +80,24 @@ def votes(n, m, batch, seed=0, faulty_mode=0, f=0, order_mode=0, order_value=1, 
     return out
 
 
+def votes2(n, m, batch, seed=0, faulty_mode=0, f=0, order_mode=0, order_value=1, first_trial=0,
+           faulty=None, order=None, threads=0):
+    """Level-2 results uint8[batch, (n-1)(n-2), n-3] of every level-1 slot (second-hop
+    split units; see ba_oracle_votes2)."""
+    lib = load()
+    faulty = None if faulty is None else np.ascontiguousarray(faulty, np.uint32)
+    order = None if order is None else np.ascontiguousarray(order, np.uint8)
+    out = np.zeros((batch, (n - 1) * (n - 2), n - 3), np.uint8)
+    rc = lib.ba_oracle_votes2(n, m, seed, faulty_mode, f, order_mode, order_value, first_trial,
+                              batch, _p(faulty), _p(order), _p(out), threads)
+    if rc != 0:
+        raise RuntimeError(f"oracle rc={rc}")
+    return out
+
+
 def pack_votes(v, jb=0, je=None):
-    """uint8[batch, L, L-1] -> the library's vote layout uint64[(je-jb)(L-1), W]."""
+    """uint8[batch, units, per-unit] -> the library's vote layout uint64[(je-jb)*per-unit, W]
+    (first-hop units: [batch, L, L-1]; second-hop units: [batch, L(L-1), L-2])."""
     batch, L, _ = v.shape
     je = L if je is None else je
     W = (batch + 63) // 64

@@ -81,6 +81,59 @@ def test_subtree_share_partitions():
         L.subtree_share(2, 1, 0)
 
 
+def test_split_share_levels():
+    """ba_split_share: level 1 is ba_subtree_share; level 2 splits the (n-1)(n-2)
+    second-hop subtrees evenly (n=16 over 8 ranks: 26/27 of 210, against 1-2 of 15
+    first hops); the second-hop split needs m_eff >= 3."""
+    from ba_amd import dist as D
+    from ba_amd import lib as L
+    for n in (4, 10, 13, 16):
+        for world in (1, 2, 3, 8):
+            assert D.split_ranges(n, 3, 1, world) == [L.subtree_share(n, world, r)
+                                                     for r in range(world)]
+    assert L.split_units(16, 5, 2) == 210 and L.split_units(16, 5, 1) == 15
+    r8 = D.split_ranges(16, 5, 2, 8)
+    assert r8[0][0] == 0 and r8[-1][1] == 210
+    assert all(b == c for (_, b), (c, _) in zip(r8, r8[1:]))
+    assert sorted({b - a for a, b in r8}) == [26, 27]
+    assert L.split_vote_slots(16, 5, 2, 0, 210) == 210 * 13  # R_2: n-3 per unit
+    assert L.split_vote_slots(16, 5, 1, 0, 15) == 15 * 14 == L.vote_slots(16, 5, 0, 15)
+    assert L.split_units(10, 2, 2) == 0 and L.split_units(10, 3, 2) == 72
+    assert L.split_units(10, 2, 3) == 0
+    with pytest.raises(L.BAError):
+        L.split_share(10, 2, 2, 2, 0)
+
+
+def test_oracle_votes2_reproduce_votes():
+    """Pins ba_oracle_votes2 on ba_oracle_votes: R_1[j.r] is the inner majority of
+    L_1[j.r] and the level-2 results R_2[j.a.r] of every other second hop a."""
+    import ctypes
+    n, m, B = 8, 4, 40
+    kw = dict(seed=7, faulty_mode=1, f=3, order_mode=1)
+    v1 = oracle_c.votes(n, m, B, **kw)
+    v2 = oracle_c.votes2(n, m, B, **kw)
+    lib = oracle_c.load()
+    L_ = n - 1
+    for t in range(B):
+        fm, oc = ctypes.c_uint32(), ctypes.c_uint8()
+        lib.ba_oracle_gen(n, 7, 1, 3, 1, 1, t, ctypes.byref(fm), ctypes.byref(oc))
+        for j in range(L_):
+            l0 = lib.ba_oracle_lie(7, t, 0, j) if fm.value & 1 else int(oc.value == 1)
+            for k in range(L_ - 1):
+                r = k + (k >= j)
+                # L_1[j.r]: lieutenant j relays L_0[j] (slot j*(L-1) + k at level 1)
+                l1 = lib.ba_oracle_lie(7, t, 1, j * (L_ - 1) + k) if (fm.value >> (j + 1)) & 1 else l0
+                a_cnt, c_cnt = l1, 1
+                for ka in range(L_ - 1):
+                    a = ka + (ka >= j)
+                    if a == r:
+                        continue
+                    others = [x for x in range(L_) if x not in (j, a)]
+                    a_cnt += int(v2[t, j * (L_ - 1) + ka, others.index(r)])
+                    c_cnt += 1
+                assert int(v1[t, j, k]) == int(2 * a_cnt > c_cnt), (t, j, r)
+
+
 # --- gloo rehearsals of the collectives' composition ------------------------------
 def _rendezvous(rank, world):
     from ba_amd import dist as D
@@ -146,6 +199,33 @@ def test_instance_split_assembles_votes(world):
     assert all(g == want for g in got)
 
 
+def _split2(rank, world):
+    """The second-hop split's exchange: every rank's ba_split_share rows of the
+    level-2 votes, assembled by gloo in place of the grouped broadcast."""
+    from ba_amd import lib as L
+    n, m, B = 9, 4, 70
+    kw = dict(seed=9, faulty_mode=1, f=3, order_mode=1, first_trial=128)
+    ub, ue = L.split_share(n, m, 2, world, rank)
+    v = oracle_c.votes2(n, m, B, **kw)
+    W = (B + 63) // 64
+    mine = oracle_c.pack_votes(v, ub, ue) if ue > ub else np.zeros((0, W), np.uint64)
+    parts = [None] * world
+    dist.all_gather_object(parts, (ub, ue, mine.tobytes()))
+    full = np.zeros((L.split_vote_slots(n, m, 2, 0, L.split_units(n, m, 2)), W), np.uint64)
+    for a, b, raw in parts:
+        if b > a:
+            full[a * (n - 3):b * (n - 3)] = np.frombuffer(raw, np.uint64).reshape(-1, W)
+    return full.tobytes()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_second_hop_split_assembles_votes(world):
+    got = spawn(_split2, world)
+    v = oracle_c.votes2(9, 4, 70, seed=9, faulty_mode=1, f=3, order_mode=1, first_trial=128)
+    want = oracle_c.pack_votes(v).tobytes()
+    assert all(g == want for g in got)
+
+
 def test_oracle_votes_reproduce_root_decisions():
     """Pins ba_oracle_votes on ba_oracle_run: the root majority of L_0[r] and the
     votes about every other first hop j is the lieutenant's decision."""
@@ -201,6 +281,46 @@ def test_subtree_votes_match_oracle_gpu(engine, n, m, B, nr):
     assert np.array_equal(dec.cpu().numpy().view(np.uint64), od)
     assert np.array_equal(out.cpu().numpy(), oo)
     assert cnt.cpu().tolist()[:COUNTERS] == list(oc.values())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,m,B,nr", [(10, 3, 200, 4), (9, 4, 130, 3), (13, 4, 65, 5),
+                                      (7, 3, 100, 3), (16, 5, 2, 8), (16, 5, 70, 8)])
+def test_second_hop_votes_match_oracle_gpu(engine, n, m, B, nr):
+    """Second-hop split (ba_split_votes_device, level 2): every rank's R_2 rows
+    (ranges from ba_split_share, starting mid first-hop subtree) equal the
+    oracle's, and the root pass over the assembled rows equals the oracle's run."""
+    from ba_amd import lib as L
+    dev = torch.device("cuda", 0)
+    kw = dict(seed=13, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1, order_mode=L.ORDER_RANDOM,
+              first_trial=64 * 5)
+    p = L.make_params(n, m, **kw)
+    W = (B + 63) // 64
+    v_or = oracle_c.votes2(n, m, B, **kw)
+    units = L.split_units(n, m, 2)
+    full = torch.zeros((L.split_vote_slots(n, m, 2, 0, units), W), dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    per = n - 3
+    for r in range(nr):
+        ub, ue = L.split_share(n, m, 2, nr, r)
+        if ue > ub:
+            engine.split_votes_device(p, B, 2, ub, ue, full[ub * per:].data_ptr(), stream=s)
+            got = full[ub * per:ue * per].cpu().numpy().view(np.uint64)
+            assert np.array_equal(got, oracle_c.pack_votes(v_or, ub, ue)), (ub, ue)
+    dec = torch.empty(B, dtype=torch.int64, device=dev)
+    out = torch.empty(B, dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(16, dtype=torch.int64, device=dev)
+    engine.root_from_split_votes_device(p, B, 2, full.data_ptr(), cnt.data_ptr(),
+                                        d_decisions=dec.data_ptr(), d_outcome=out.data_ptr(),
+                                        stream=s)
+    torch.cuda.synchronize()
+    od, oo, oc = oracle_c.run(n, m, B, **kw)
+    assert np.array_equal(dec.cpu().numpy().view(np.uint64), od)
+    assert np.array_equal(out.cpu().numpy(), oo)
+    assert cnt.cpu().tolist()[:COUNTERS] == list(oc.values())
+    with pytest.raises(L.BAError) as ei:  # m_eff < 3: no second-hop split
+        engine.split_votes_device(L.make_params(10, 2, **kw), B, 2, 0, 1, full.data_ptr())
+    assert ei.value.code == L.ENOTSUP
 
 
 @pytest.mark.gpu

@@ -8,8 +8,9 @@ does the rendezvous).
   3  n=13, m=4, 64M trials, trial-DP across ranks (counters all-reduced)
   4  n=10, m=3 faulty-count sweep f = 0..n/3+1, exactly f faulty, 1M trials each:
      agreement (IC1) / validity (IC2) / quorum-outcome breakdown curve
-  5  n=16, m=5: one instance split by first-hop subtree (latency), and a batch
-     of 1024 instances (throughput), votes all-gathered across ranks
+  5  n=16, m=5: one instance split by first-hop subtree (--split-level 2:
+     second-hop subtree) (latency), and a batch of 1024 instances (throughput),
+     votes all-gathered across ranks
 
 Rank 0 prints one JSON line per config.  Timings bracket the device work with
 torch.cuda.synchronize() (+ a gloo barrier across ranks) and take the max over
@@ -58,6 +59,8 @@ def main():
     ap.add_argument("--trials3", type=int, default=64 << 20)
     ap.add_argument("--trials4", type=int, default=1 << 20)
     ap.add_argument("--batch5", type=int, default=1024)
+    ap.add_argument("--split-level", type=int, default=1,
+                    help="config 5 split: 1 = first-hop subtrees, 2 = second-hop subtrees")
     a = ap.parse_args()
     which = {int(x) for x in a.only.split(",")}
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -104,14 +107,15 @@ def main():
         for B in (1, a.batch5):
             p = L.make_params(n, m, 0xBA5EED, L.LIE_PHILOX, L.FAULTY_RANDOM, 5, L.ORDER_RANDOM,
                               L.ATTACK, L.ENGINE_LEVELS, 0)
-            D.run_instance_split(comm, p, B, dev)  # warm-up
+            lv = a.split_level
+            D.run_instance_split(comm, p, B, dev, level=lv)  # warm-up
             reps = 10 if B == 1 else 3
-            (dec, o, cnt), dt = timed(lambda: [D.run_instance_split(comm, p, B, dev)
+            (dec, o, cnt), dt = timed(lambda: [D.run_instance_split(comm, p, B, dev, level=lv)
                                                for _ in range(reps)][-1], world, dev)
             res[B] = {"seconds_per_call": dt / reps, "instances_per_s": B * reps / dt,
                       "counters": counters(cnt)}
             # the same call replayed from hipGraphs (D.InstanceSplitGraphs, its own ctx)
-            g = D.InstanceSplitGraphs(dev, p, B, comm if world > 1 else None)
+            g = D.InstanceSplitGraphs(dev, p, B, comm if world > 1 else None, level=lv)
             reps_g = 50 if B == 1 else 10
             (gd, go, gc), gdt = timed(lambda: [g.replay() for _ in range(reps_g)][-1], world, dev)
             if not (torch.equal(gd, dec) and torch.equal(go, o) and counters(gc) == counters(cnt)):
@@ -119,8 +123,9 @@ def main():
             res[B]["graph_seconds_per_call"] = gdt / reps_g
             res[B]["graph_instances_per_s"] = B * reps_g / gdt
             g.close()
-        out.append({"config": 5, "workload": f"OM({m}) n={n} (3,999,675 tree slots), first-hop "
-                    f"subtree split over {world} GPU(s), votes all-gathered",
+        out.append({"config": 5, "workload": f"OM({m}) n={n} (3,999,675 tree slots), "
+                    f"{'first' if a.split_level == 1 else 'second'}-hop subtree split over "
+                    f"{world} GPU(s), votes all-gathered", "split_level": a.split_level,
                     "latency_one_instance_ms": res[1]["seconds_per_call"] * 1e3,
                     "latency_one_instance_ms_graph": res[1]["graph_seconds_per_call"] * 1e3,
                     "batch": a.batch5, "throughput_instances_per_s": res[a.batch5]["instances_per_s"],
