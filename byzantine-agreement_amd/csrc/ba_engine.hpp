@@ -136,6 +136,15 @@ hipError_t launch_leaf(const Geometry& g, uint64_t seed, uint64_t gw0, uint32_t 
 hipError_t launch_fused(const RunArgs& a, const Geometry& g, bool plan_ok, const FusedPlan& fp,
                         const FusedPlan* d_fp, const uint8_t* d_sender, uint64_t* partials);
 
+// LEVELS small-batch tail (ba_tail.hip): level-1 majorities + roots + quorum
+// of W <= kTailMaxWords words in one launch (config 5 A/B, one call: -3 us at
+// 1 and 16 instances, neutral at 16 words = 1024 instances)
+constexpr uint32_t kTailMaxWords = 16;
+bool tail_supported(const Geometry& g);
+hipError_t launch_tail(const RunArgs& a, const Geometry& g, uint64_t W, const uint64_t* scratch,
+                       const LevelsLayout& lay, const uint64_t* L1, const uint64_t* C2,
+                       uint32_t c2base, uint64_t* decisions, uint8_t* outcome);
+
 hipError_t launch_table(const RunArgs& a, uint64_t* partials);
 hipError_t launch_gen_inputs(const RunArgs& a, uint32_t* faulty_out, uint8_t* order_out);
 hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_t* d_sender,

@@ -276,11 +276,15 @@ struct TopPlan {
     FastDiv D[kTopMax + 1];            // D[k] = prod_{i=k+1..K} (L - i): level-K slots per level-k slot
 };
 
-// Inputs fused in (IN.fuse, batches of at most kTopFuseWords words): every block
-// bit-slices the batch's inputs itself into LDS (a wave per word) and reads F /
-// OB from there, and block 0 also stores them to scratch for the later kernels
-// -- one launch (k_input) less on the latency-bound small batches of config 5.
-constexpr uint32_t kTopFuseWords = 2;  // every block re-slices the inputs: small batches only
+// Inputs fused in (IN.fuse): every block bit-slices the batch's inputs itself
+// into LDS (a wave per word) and reads F / OB from there, and block 0 also
+// stores them to scratch for the later kernels -- one launch (k_input) less on
+// the latency-bound small batches of config 5.  Every block re-slices the
+// whole batch, so this pays only for tiny batches: at 16 words (config 5's
+// 1024 instances) the fused launch measured 4.6 us slower per call than
+// k_input + k_relay_top, with staged and with drawn inputs (tools/config5_ab.py).
+constexpr uint32_t kTopFuseWords = 2;
+constexpr uint32_t kTopFuseGivenWords = kTopFuseWords;
 struct TopInputs {
     uint32_t fuse, n;
     uint64_t seed, t0, ntrials;
@@ -290,6 +294,49 @@ struct TopInputs {
     uint64_t offOO, offVAL;
 };
 
+// The ancestor chain of level-K slot x: levels 0..K-1, each a relay of the
+// one above (commander first), drawn from the Philox pair of the ancestor's
+// global slot pair (k_relay's keying, so the bits are identical).  Returns
+// the value of x's level K-1 ancestor and writes every ancestor x is the first
+// descendant of.  All table and F loads are issued before the first store (a
+// store to scratch may alias F, so interleaving them would serialise one
+// memory round trip per level), and the K Philox calls -- plus, with EXTRA,
+// the caller's level-K pair `xc` -- run as one interleaved group.
+template <int K, bool EXTRA>
+__device__ __forceinline__ uint64_t top_chain(const TopPlan& tp, uint32_t x, uint32_t w,
+                                              uint32_t W, uint64_t gw, uint64_t seed,
+                                              const uint64_t* F, uint64_t ob,
+                                              const uint8_t* __restrict__ sender,
+                                              uint64_t* __restrict__ scratch, P4& xc) {
+    uint32_t a[K], snd[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] = fdiv(x, tp.D[k]);
+    snd[0] = 0;  // level 0: the commander relays
+#pragma unroll
+    for (int k = 1; k < K; ++k) snd[k] = sender[tp.snd_off[k - 1] + a[k - 1]];
+    uint64_t fw[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) fw[k] = F[(uint64_t)snd[k] * W + w];
+    constexpr int G = K + (EXTRA ? 1 : 0);
+    P4 c[G];
+#pragma unroll
+    for (int k = 0; k < K; ++k) c[k] = P4{a[k] >> 1, (uint32_t)k, (uint32_t)gw, (uint32_t)(gw >> 32)};
+    if constexpr (EXTRA) c[K] = xc;
+    philox10_n<G>(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    if constexpr (EXTRA) xc = c[K];
+    uint64_t v = ob;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint64_t lie = (a[k] & 1u) ? ((uint64_t)c[k].w << 32 | c[k].z)
+                                         : ((uint64_t)c[k].y << 32 | c[k].x);
+        v = (fw[k] & lie) | (~fw[k] & v);
+        if (k >= 1 && x == a[k] * tp.D[k].d)  // first descendant writes the ancestor
+            scratch[tp.off[k] + (uint64_t)(a[k] - tp.base[k]) * W + w] = v;
+    }
+    return v;
+}
+
+template <int K>
 __global__ __launch_bounds__(kBlock) void k_relay_top(TopPlan tp, FastDiv divW, uint32_t work,
                                                       uint64_t seed, uint64_t gw0,
                                                       const uint8_t* __restrict__ sender,
@@ -299,13 +346,10 @@ __global__ __launch_bounds__(kBlock) void k_relay_top(TopPlan tp, FastDiv divW, 
     const uint32_t work0 = tp.np0 * W;
     const uint64_t* F = scratch + offF;
     const uint64_t* OBp = scratch + offOB;
-    __shared__ uint64_t sIn[kTopFuseWords * (kMaxN + 1)];  // F[g][w] rows, then OB[w]
+    __shared__ uint64_t sIn[kTopFuseGivenWords * (kMaxN + 1)];  // F[g][w] rows, then OB[w]
     if (IN.fuse) {
-        const uint32_t lane = threadIdx.x & 63;
-        for (uint32_t w = threadIdx.x >> 6; w < W; w += kBlock / 64) {
-            uint64_t mine, ob, oo, vv;
-            word_inputs(IN.n, IN.seed, IN.gs, IN.t0, IN.ntrials, IN.faulty, IN.order, w, lane, mine,
-                        ob, oo, vv);
+        const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        auto put = [&](uint32_t w, uint64_t mine, uint64_t ob, uint64_t oo, uint64_t vv) {
             if (lane < IN.n) sIn[lane * W + w] = mine;
             if (lane == 0) sIn[IN.n * W + w] = ob;
             if (blockIdx.x == 0) {
@@ -315,6 +359,42 @@ __global__ __launch_bounds__(kBlock) void k_relay_top(TopPlan tp, FastDiv divW, 
                     scratch[IN.offOO + w] = oo;
                     scratch[IN.offVAL + w] = vv;
                 }
+            }
+        };
+        if (IN.gs.faulty_mode == 0 && IN.gs.order_mode == 0) {
+            // given (staged) inputs: every load of the wave's words in flight
+            // before the first ballot (a load-ballot loop waits one round trip
+            // per word)
+            constexpr uint32_t PW = (kTopFuseGivenWords + kBlock / 64 - 1) / (kBlock / 64);
+            uint32_t fm[PW], oc[PW];
+#pragma unroll
+            for (uint32_t j = 0; j < PW; ++j) {
+                const uint32_t w = wv + j * (kBlock / 64);
+                const uint64_t i = (uint64_t)w * 64 + lane;
+                const bool ok = w < W && i < IN.ntrials;
+                fm[j] = ok ? IN.faulty[i] : 0u;
+                oc[j] = ok ? IN.order[i] : 0u;
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < PW; ++j) {
+                const uint32_t w = wv + j * (kBlock / 64);
+                if (w >= W) break;
+                const uint64_t i = (uint64_t)w * 64 + lane;
+                const bool valid = i < IN.ntrials;
+                uint64_t mine = 0;
+                for (uint32_t g = 0; g < IN.n; ++g) {
+                    const uint64_t b = __ballot(valid && ((fm[j] >> g) & 1u));
+                    if (lane == g) mine = b;
+                }
+                put(w, mine, __ballot(valid && oc[j] == 1), __ballot(valid && oc[j] == 2),
+                    __ballot(valid));
+            }
+        } else {
+            for (uint32_t w = wv; w < W; w += kBlock / 64) {
+                uint64_t mine, ob, oo, vv;
+                word_inputs(IN.n, IN.seed, IN.gs, IN.t0, IN.ntrials, IN.faulty, IN.order, w, lane,
+                            mine, ob, oo, vv);
+                put(w, mine, ob, oo, vv);
             }
         }
         __syncthreads();
@@ -334,39 +414,32 @@ __global__ __launch_bounds__(kBlock) void k_relay_top(TopPlan tp, FastDiv divW, 
             }
             continue;
         }
-        const uint32_t it = idx - work0;
-        const uint32_t pl = fdiv(it, divW), w = it - pl * W;
-        const uint64_t gw = gw0 + w;
-        const uint32_t pairK = (tp.xbK >> 1) + pl;
-        uint64_t lieK[2];
-        lie_pair(seed, tp.K, pairK, gw, lieK[0], lieK[1]);
-        const uint64_t ob = OBp[w];
-        uint32_t prev_parent = 0xFFFFFFFFu;
-        uint64_t parent_val = 0;
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t x = 2 * pairK + h;
-            if (x < tp.xbK || x >= tp.xeK) continue;
-            const uint32_t par = fdiv(x, tp.D[tp.K - 1]);  // level K-1 ancestor
-            if (par != prev_parent) {  // walk the chain levels 0..K-1 (once per parent)
-                uint64_t v = ob;
-#pragma unroll
-                for (int k = 0; k < kTopMax; ++k) {
-                    if (k >= (int)tp.K) break;
-                    const uint32_t a = fdiv(x, tp.D[k]);
-                    const uint64_t fw = k == 0 ? F[w]
-                                               : F[(uint64_t)sender[tp.snd_off[k - 1] + fdiv(x, tp.D[k - 1])] * W + w];
-                    uint64_t l2[2];
-                    lie_pair(seed, (uint32_t)k, a >> 1, gw, l2[0], l2[1]);
-                    v = (fw & l2[a & 1u]) | (~fw & v);
-                    if (k >= 1 && x == a * tp.D[k].d)  // first descendant writes the ancestor
-                        scratch[tp.off[k] + (uint64_t)(a - tp.base[k]) * W + w] = v;
+        if constexpr (K >= 1) {
+            const uint32_t it = idx - work0;
+            const uint32_t pl = fdiv(it, divW), w = it - pl * W;
+            const uint64_t gw = gw0 + w;
+            const uint32_t pairK = (tp.xbK >> 1) + pl;
+            const uint32_t x0 = 2 * pairK, x1 = x0 + 1;
+            const bool ok0 = x0 >= tp.xbK && x0 < tp.xeK, ok1 = x1 >= tp.xbK && x1 < tp.xeK;
+            const uint32_t xa = ok0 ? x0 : x1;  // chain anchor: the first slot of the range
+            const uint32_t par0 = fdiv(x0, tp.D[K - 1]), par1 = fdiv(x1, tp.D[K - 1]);
+            const uint32_t para = ok0 ? par0 : par1;
+            // level-K senders (loads issued before the chain's stores)
+            const uint64_t fw0 = ok0 ? F[(uint64_t)sender[tp.snd_off[K - 1] + par0] * W + w] : 0ull;
+            const uint64_t fw1 = ok1 ? F[(uint64_t)sender[tp.snd_off[K - 1] + par1] * W + w] : 0ull;
+            const uint64_t ob = OBp[w];
+            P4 xc{pairK, (uint32_t)K, (uint32_t)gw, (uint32_t)(gw >> 32)};
+            const uint64_t va = top_chain<K, true>(tp, xa, w, W, gw, seed, F, ob, sender, scratch, xc);
+            const uint64_t lieK0 = (uint64_t)xc.y << 32 | xc.x, lieK1 = (uint64_t)xc.w << 32 | xc.z;
+            if (ok0) scratch[tp.off[K] + (uint64_t)(x0 - tp.base[K]) * W + w] = (fw0 & lieK0) | (~fw0 & va);
+            if (ok1) {
+                uint64_t v1 = va;
+                if (par1 != para) {  // the pair straddles two parents (odd L-K only): second chain
+                    P4 none{};
+                    v1 = top_chain<K, false>(tp, x1, w, W, gw, seed, F, ob, sender, scratch, none);
                 }
-                prev_parent = par;
-                parent_val = v;
+                scratch[tp.off[K] + (uint64_t)(x1 - tp.base[K]) * W + w] = (fw1 & lieK1) | (~fw1 & v1);
             }
-            const uint64_t fw = F[(uint64_t)sender[tp.snd_off[tp.K - 1] + par] * W + w];
-            scratch[tp.off[tp.K] + (uint64_t)(x - tp.base[tp.K]) * W + w] =
-                (fw & lieK[h]) | (~fw & parent_val);
         }
     }
 }
@@ -638,7 +711,9 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
     // small batches: the inputs are bit-sliced inside k_relay_top (TopInputs)
     const bool no_fuse_in = getenv("BA_NO_INPUT_FUSION") && atoi(getenv("BA_NO_INPUT_FUSION")) != 0;
     TopInputs tin{};
-    tin.fuse = (!no_fuse_in && W <= kTopFuseWords && a.n <= (uint32_t)kMaxN) ? 1u : 0u;
+    const bool given_in = a.gen.faulty_mode == 0 && a.gen.order_mode == 0;
+    tin.fuse = (!no_fuse_in && a.n <= (uint32_t)kMaxN &&
+                W <= (given_in ? kTopFuseGivenWords : kTopFuseWords)) ? 1u : 0u;
     tin.n = a.n;
     tin.seed = a.seed;
     tin.t0 = a.first_trial + trial0;
@@ -703,9 +778,17 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
         const uint32_t npK = kf == 0 ? 0u : (tp.xeK + 1) / 2 - tp.xbK / 2;
         const uint32_t work = (uint32_t)((uint64_t)(tp.np0 + (tp.xeK > tp.xbK ? npK : 0u)) * W);
         ProfScope ps(a.prof, "k_relay_top", st);
-        hipLaunchKernelGGL(k_relay_top, dim3(blocks_for(work, 16384)), dim3(kBlock), 0, st, tp,
-                           make_fastdiv((uint32_t)W), work, a.seed, gw0, d_sender, scratch, lay.F,
-                           lay.OB, tin);
+        const dim3 grid(blocks_for(work, 16384)), blk(kBlock);
+        const FastDiv dW = make_fastdiv((uint32_t)W);
+        switch (kf) {
+#define BA_TOP(KK)                                                                               \
+    case KK:                                                                                     \
+        hipLaunchKernelGGL(k_relay_top<KK>, grid, blk, 0, st, tp, dW, work, a.seed, gw0, d_sender, \
+                           scratch, lay.F, lay.OB, tin);                                         \
+        break;
+            BA_TOP(0) BA_TOP(1) BA_TOP(2) BA_TOP(3) BA_TOP(4) BA_TOP(5) BA_TOP(6)
+#undef BA_TOP
+        }
         if ((e = hipGetLastError()) != hipSuccess) return e;
         k_first = kf + 1;
     }
@@ -747,7 +830,11 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
     // over the gathered votes
     const int pdeep = job.tree ? (int)g.me - (lay.leaf_fused ? (leaf_up ? 3 : 2) : 1) : (int)job.h - 1;
     const int plow = (job.tree && job.votes_out) ? (int)job.h : 1;
-    for (int p = pdeep; p >= plow; --p) {
+    // small batches: level 1 + roots + quorum in one k_tail launch (level 1 whole)
+    const bool no_tail = getenv("BA_NO_TAIL") && atoi(getenv("BA_NO_TAIL")) != 0;
+    const bool tail = !no_tail && job.root && plow == 1 && pdeep >= 1 && W <= kTailMaxWords &&
+                      tail_supported(g) && lay.base[1] == 0 && lay.cnt[1] == g.S[1];
+    for (int p = pdeep; p >= (tail ? 2 : plow); --p) {
         const uint32_t s = g.L - (uint32_t)p;
         const uint32_t work = (uint32_t)(lay.cnt[p] * W);
         const uint32_t ybase = (uint32_t)lay.base[p], cbase = (uint32_t)lay.base[p + 1];
@@ -766,6 +853,14 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (!job.root) return hipSuccess;
+    if (tail) {
+        const uint64_t* C2 = (!job.tree && job.h == 2) ? job.votes_in
+                             : (g.me == 2 ? Lptr(2) : Rptr(2));
+        ProfScope ps(a.prof, "k_tail", st);
+        return launch_tail(a, g, W, scratch, lay, Lptr(1), C2, (uint32_t)lay.base[2],
+                           a.decisions ? a.decisions + trial0 : nullptr,
+                           a.outcome ? a.outcome + trial0 : nullptr);
+    }
     // root + quorum epilogue over L_0 and the level-1 child results
     const uint64_t* C1 = (job.votes_in && job.h == 1) ? job.votes_in
                          : (g.me >= 2 ? scratch + lay.Rp[1] : (g.me == 1 ? scratch + lay.Lk[1] : nullptr));

@@ -310,8 +310,11 @@ __device__ __forceinline__ uint32_t popc_t(T x) {
     else return (uint32_t)__popc(x);
 }
 
+// ME = 0: the effective depth is the runtime me_rt (the LEVELS tail, any tree of
+// N generals); it only sets the in-bound flag, taken from the resolved planes.
 template <int N, uint32_t ME, typename T, typename In, typename Au, typename Out>
-__device__ __forceinline__ void epilogue_core(In in, Au au, Out out, TrialCounts& tc) {
+__device__ __forceinline__ void epilogue_core(In in, Au au, Out out, TrialCounts& tc,
+                                              uint32_t me_rt = ME) {
     constexpr int L = N - 1, NB = planes_c(N);
     // an odd number of root inputs never ties: no undefined decisions, U == 0
     constexpr bool TIES = L % 2 == 0;
@@ -353,7 +356,22 @@ __device__ __forceinline__ void epilogue_core(In in, Au au, Out out, TrialCounts
     const T agree = TIES ? ~maj3(anyA, anyU, anyR) : ~(anyA & anyR);
     const T appl = ~f0;
     const T valid = appl & ((ob & allA) | (~ob & allR));
-    const T inb = (N > 3 * (int)ME) ? ~cF.template ge<N, (int)ME + 1>() : (T)0;
+    T inb = (T)0;
+    if constexpr (ME > 0) {
+        inb = (N > 3 * (int)ME) ? ~cF.template ge<N, (int)ME + 1>() : (T)0;
+    } else if ((uint32_t)N > 3 * me_rt) {  // inb = faulty count <= me_rt, from the count planes
+        const uint32_t th = me_rt + 1;
+        T gt = 0, eq = (T)~(T)0;
+        static_for<0, NB>([&](auto j) {
+            constexpr int i = NB - 1 - j();
+            if ((th >> i) & 1u) eq &= rF[i];
+            else {
+                gt |= eq & rF[i];
+                eq &= ~rF[i];
+            }
+        });
+        inb = (th >> NB) ? (T)~(T)0 : ~(gt | eq);
+    }
     tc.v[C_TRIALS] += popc_t<T>(val);
     tc.v[C_AGREE] += popc_t<T>(agree & val);
     tc.v[C_VAPPL] += popc_t<T>(appl & val);
@@ -381,19 +399,20 @@ __device__ __forceinline__ void epilogue_core(In in, Au au, Out out, TrialCounts
 // only its own byte k).
 template <int N, uint32_t ME>
 __device__ __forceinline__ void epilogue_byte(uint64_t* inw, const uint64_t* au, uint32_t k,
-                                              TrialCounts& tc) {
+                                              TrialCounts& tc, uint32_t me_rt = ME) {
     uint8_t* ib = reinterpret_cast<uint8_t*>(inw) + k;
     const uint8_t* ab = reinterpret_cast<const uint8_t*>(au) + k;
     epilogue_core<N, ME, uint32_t>([&](int p) -> uint32_t { return ib[8 * p]; },
                                    [&](int b) -> uint32_t { return ab[8 * b]; },
-                                   [&](int o, uint32_t v) { ib[8 * o] = (uint8_t)v; }, tc);
+                                   [&](int o, uint32_t v) { ib[8 * o] = (uint8_t)v; }, tc, me_rt);
 }
 
 template <int N, int W, uint32_t ME, int DIAG>
 __device__ __forceinline__ void wave_epilogue(uint64_t* in0, const uint64_t* au0,
                                               uint32_t lane, uint64_t w0, uint64_t batch,
                                               uint64_t* __restrict__ decisions,
-                                              uint8_t* __restrict__ outcome, TrialCounts& tc) {
+                                              uint8_t* __restrict__ outcome, TrialCounts& tc,
+                                              uint32_t me_rt = ME) {
     constexpr int L = N - 1, NIN = N + 3;
     static_assert(L <= 16, "decision word: 2 bits per lieutenant in the low 32 bits");
     if constexpr ((DIAG & 32) != 0) {  // lab: near-free stand-in epilogue
@@ -404,7 +423,7 @@ __device__ __forceinline__ void wave_epilogue(uint64_t* in0, const uint64_t* au0
         return;
     }
     for (uint32_t it = lane; it < (uint32_t)W * 8; it += 64)
-        epilogue_byte<N, ME>(in0 + (it >> 3) * NIN, au0 + (it >> 3) * 2 * L, it & 7u, tc);
+        epilogue_byte<N, ME>(in0 + (it >> 3) * NIN, au0 + (it >> 3) * 2 * L, it & 7u, tc, me_rt);
     __builtin_amdgcn_wave_barrier();
     const uint32_t half = lane >> 5, sh = lane & 31;
     auto bit = [&](const uint64_t* p) -> uint32_t {

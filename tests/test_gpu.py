@@ -517,13 +517,18 @@ def test_run_trials_multi_world1_rccl(engine):
 
 
 @pytest.mark.parametrize("n,m,B", [(16, 5, 100), (16, 5, 1), (10, 3, 64 * 64), (10, 3, 64 * 64 + 1),
-                                   (7, 2, 5), (13, 4, 64 * 20 + 9), (9, 5, 130)])
+                                   (7, 2, 5), (13, 4, 64 * 20 + 9), (9, 5, 130), (16, 5, 1024),
+                                   (16, 3, 300), (16, 2, 70), (12, 4, 200)])
 def test_levels_small_batch_fusions_vs_oracle(monkeypatch, n, m, B):
     """LEVELS launch fusions on and off -- the inputs bit-sliced inside
-    k_relay_top (batches up to 2 words) vs the k_input launch, and k_leaf taking
+    k_relay_top (batches up to 2 words) vs the k_input launch, k_leaf taking
     the level me-2 majority itself (leaf-up, m_eff >= 3) vs writing R_{me-1} for
-    a k_majority launch (BA_NO_INPUT_FUSION / BA_NO_LEAF_UP = 1): every
-    combination equals the oracle, for drawn and given inputs."""
+    a k_majority launch, and the small-batch k_tail (level 1 + roots + quorum,
+    up to 16 words) vs k_majority + k_epilogue (BA_NO_INPUT_FUSION /
+    BA_NO_LEAF_UP / BA_NO_TAIL = 1): every combination equals the oracle, for
+    drawn and given inputs.  (16, 3) and (16, 2) run without leaf fusion (the
+    tail then reads R_2 / the leaves L_2); (12, 4) and (9, 5) have relay pairs
+    that straddle two parents in k_relay_top."""
     from ba_amd import lib as L
     kw = dict(seed=0xFACE + n, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1,
               order_mode=L.ORDER_RANDOM, first_trial=64 * 9)
@@ -532,10 +537,12 @@ def test_levels_small_batch_fusions_vs_oracle(monkeypatch, n, m, B):
     fm = rng.integers(0, 1 << n, B, dtype=np.uint64).astype(np.uint32)
     oc = rng.choice([0, 1, 2], B).astype(np.uint8)
     gd, go, gcnt = oracle_c.run(n, m, B, seed=3, faulty=fm, order=oc)
-    for off_in, off_up in (("0", "0"), ("1", "1"), ("0", "1"), ("1", "0")):
-        off = off_in + off_up
+    for off_in, off_up, off_tail in (("0", "0", "0"), ("1", "1", "1"), ("0", "1", "0"),
+                                     ("1", "0", "1"), ("0", "0", "1"), ("1", "1", "0")):
+        off = off_in + off_up + off_tail
         monkeypatch.setenv("BA_NO_INPUT_FUSION", off_in)
         monkeypatch.setenv("BA_NO_LEAF_UP", off_up)
+        monkeypatch.setenv("BA_NO_TAIL", off_tail)
         e = L.Engine(0)
         try:
             res = e.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)

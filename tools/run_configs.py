@@ -123,6 +123,37 @@ def main():
             res[B]["graph_seconds_per_call"] = gdt / reps_g
             res[B]["graph_instances_per_s"] = B * reps_g / gdt
             g.close()
+            if world == 1:
+                # sustained stream of calls, inputs staged in HBM before timing (as
+                # bench.py): the same instances, every call launched back to back on
+                # one stream (no host sync between calls; the unsplit pass is what
+                # the one-rank split runs)
+                fb = torch.empty(B, dtype=torch.int32, device=dev)
+                ob = torch.empty(B, dtype=torch.uint8, device=dev)
+                st = torch.cuda.Stream(dev)
+                eng.gen_inputs_device(p, B, d_faulty=fb.data_ptr(), d_order=ob.data_ptr(),
+                                      stream=st.cuda_stream)
+                pg = L.make_params(n, m, 0xBA5EED, L.LIE_PHILOX, L.FAULTY_GIVEN, 5, L.ORDER_GIVEN,
+                                   L.ATTACK, L.ENGINE_LEVELS, 0)
+                sd = torch.empty(B, dtype=torch.int64, device=dev)
+                so = torch.empty(B, dtype=torch.uint8, device=dev)
+                sc = torch.zeros(16, dtype=torch.int64, device=dev)
+
+                def call():
+                    eng.run_device(pg, B, d_faulty=fb.data_ptr(), d_order=ob.data_ptr(),
+                                   d_decisions=sd.data_ptr(), d_outcome=so.data_ptr(),
+                                   d_counters=sc.data_ptr(), stream=st.cuda_stream)
+                call()  # warm-up (geometry, scratch)
+                torch.cuda.synchronize(dev)
+                sc.zero_()
+                call()
+                torch.cuda.synchronize(dev)
+                if not (torch.equal(sd, dec) and torch.equal(so, o) and counters(sc) == counters(cnt)):
+                    raise SystemExit("config 5: staged-input call differs from the split")
+                reps_s = 20 if B == 1 else 50
+                _, sdt = timed(lambda: [call() for _ in range(reps_s)], world, dev)
+                res[B]["stream_seconds_per_call"] = sdt / reps_s
+                res[B]["stream_instances_per_s"] = B * reps_s / sdt
         out.append({"config": 5, "workload": f"OM({m}) n={n} (3,999,675 tree slots), "
                     f"{'first' if a.split_level == 1 else 'second'}-hop subtree split over "
                     f"{world} GPU(s), votes all-gathered", "split_level": a.split_level,
@@ -130,6 +161,10 @@ def main():
                     "latency_one_instance_ms_graph": res[1]["graph_seconds_per_call"] * 1e3,
                     "batch": a.batch5, "throughput_instances_per_s": res[a.batch5]["instances_per_s"],
                     "throughput_instances_per_s_graph": res[a.batch5]["graph_instances_per_s"],
+                    "latency_one_instance_ms_stream": res[1].get("stream_seconds_per_call", 0) * 1e3,
+                    "throughput_instances_per_s_stream": res[a.batch5].get("stream_instances_per_s"),
+                    "stream_note": "staged inputs, calls launched back to back on one stream "
+                                   "(one rank only)",
                     "n_gpus": world, "counters_batch": res[a.batch5]["counters"]})
 
     if rank == 0:
