@@ -17,8 +17,12 @@ steps, so neither pays the clock ramp.
 N>1: launched one process per GPU by torch.distributed.run.  Trials shard by
 global index (weak scaling, no data-path collective); the run counters are
 all-reduced once over RCCL inside the C ABI (ba_comm_allreduce_device) at the
-end of the timed region.  torch.distributed (gloo) is the rendezvous only: the
-RCCL unique id, the barriers and the max-over-ranks of the wall time.
+end of the timed region, and that all-reduce is the closing barrier (it ends
+on a rank only after every rank's steps have ended); the opening barrier is a
+gloo barrier followed by an RCCL all-reduce of a dummy buffer, so the ranks
+leave it together.  torch.distributed (gloo) carries the RCCL unique id and
+the max-over-ranks of the wall time.  (A gloo barrier inside the timed region
+would add a host TCP round trip to a ~1 ms region.)
 
 Prints ONE JSON line (rank 0).  DESIGN.md §5 gives the roofline accounting:
 `roofline` is the dominant kernel's HBM roofline on the bytes it must move
@@ -220,6 +224,10 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")  # rendezvous, barriers, wall-time max; RCCL is in the C ABI
+    # BA_BENCH_DEVICE: put every rank on one device (a multi-rank rehearsal on a
+    # one-GPU box; RCCL refuses two ranks on one GPU, so the counters then go
+    # through the gloo fallback)
+    local = int(os.environ.get("BA_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     n, m, B = args.n, args.m, args.batch
@@ -295,11 +303,15 @@ def main():
             break
     warm_s = time.perf_counter() - t_w
 
+    bar = torch.zeros(16, dtype=torch.int64, device=dev)  # RCCL barrier operand
+
     def timed(base, in_kernel):
         cnt.zero_()
         torch.cuda.synchronize(dev)
         if dist:
             dist.barrier()
+            if comm is not None:  # release every rank together: a device-side RCCL barrier
+                comm.allreduce_device(bar.data_ptr(), stream=sp)
         torch.cuda.synchronize(dev)
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
@@ -309,13 +321,14 @@ def main():
             step(base + i, in_kernel)
         ev1.record(stream)
         if comm is not None:
-            comm.allreduce_device(cptr, stream=sp)  # the only collective: run counters (RCCL)
+            # the only collective: the run counters (RCCL).  It is also the closing
+            # barrier: it completes on a rank only after every rank's steps ended.
+            comm.allreduce_device(cptr, stream=sp)
         torch.cuda.synchronize(dev)
-        if dist and comm is None:
+        if dist and comm is None:  # gloo fallback: host all-reduce, then a host barrier
             host = cnt.cpu()
             dist.all_reduce(host)
             cnt.copy_(host)
-        if dist:
             dist.barrier()
         wall = time.perf_counter() - t0
         elapsed = torch.tensor([wall], dtype=torch.float64)

@@ -163,8 +163,21 @@ __host__ __device__ __forceinline__ P4 philox10(P4 c, uint32_t k0, uint32_t k1) 
 // source order interleaves the chains, so each v_mad_u64_u32 result is used G
 // instructions later instead of right away (left to itself the scheduler runs
 // the calls one after another and exposes the multiply latency).
+#if defined(__HIP_DEVICE_COMPILE__) && defined(BA_PHILOX_VKEYS)
+// lab: the round keys as VGPR operands of the xor3s (the compiler sees them as
+// divergent values, so it keeps them in VGPRs instead of SGPRs)
+__device__ __forceinline__ uint32_t as_vgpr(uint32_t k) {
+    uint32_t r;
+    asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(k));
+    return r;
+}
+#endif
 template <int G>
 __host__ __device__ __forceinline__ void philox10_n(P4 (&c)[G], uint32_t k0, uint32_t k1) {
+#if defined(__HIP_DEVICE_COMPILE__) && defined(BA_PHILOX_VKEYS)
+    k0 = as_vgpr(k0);
+    k1 = as_vgpr(k1);
+#endif
     static_for_h<0, 10>([&](auto i) {
         uint64_t p0[G], p1[G];
         philox_mul2_n<i(), G>(c, p0, p1);

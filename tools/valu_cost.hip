@@ -11,9 +11,11 @@
 #include <cstdio>
 #include <vector>
 
-enum Op { XOR3, ADD, MAD64, MULLO, MULHI, BFI, MAD24, LSHL_OR };
+enum Op { XOR3, ADD, MAD64, MULLO, MULHI, BFI, MAD24, LSHL_OR, XOR3_V, MAD64_V, ADD_S, ADD3_V };
 static const char* kNames[] = {"v_bitop3_b32(xor3)", "v_add_u32", "v_mad_u64_u32", "v_mul_lo_u32",
-                               "v_mul_hi_u32", "v_bfi_b32", "v_mad_u32_u24", "v_lshl_or_b32"};
+                               "v_mul_hi_u32", "v_bfi_b32", "v_mad_u32_u24", "v_lshl_or_b32",
+                               "v_bitop3_b32(xor3, all VGPR)", "v_mad_u64_u32(VGPR multiplier)",
+                               "v_add_u32(SGPR src0)", "v_add3_u32(all VGPR)"};
 constexpr int CH = 16;
 
 // One asm statement issues the instruction once on each of 8 independent
@@ -57,6 +59,27 @@ __device__ __forceinline__ void op8(uint32_t (&a)[8], uint64_t (&r)[8], uint32_t
                      : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
                        "+v"(a[6]), "+v"(a[7])
                      : "v"(x), "s"(m));
+    } else if constexpr (OP == XOR3_V) {
+        asm volatile("v_bitop3_b32 %0, %0, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %1, %1, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %2, %2, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %3, %3, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %4, %4, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %5, %5, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %6, %6, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %7, %7, %8, %9 bitop3:0x96"
+                     : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
+                       "+v"(a[6]), "+v"(a[7])
+                     : "v"(x), "v"(m));
+    } else if constexpr (OP == MAD64_V) {
+        uint64_t cc;
+        asm volatile("v_mad_u64_u32 %0, %8, %9, %10, %0\n\tv_mad_u64_u32 %1, %8, %9, %10, %1\n\tv_mad_u64_u32 %2, %8, %9, %10, %2\n\tv_mad_u64_u32 %3, %8, %9, %10, %3\n\tv_mad_u64_u32 %4, %8, %9, %10, %4\n\tv_mad_u64_u32 %5, %8, %9, %10, %5\n\tv_mad_u64_u32 %6, %8, %9, %10, %6\n\tv_mad_u64_u32 %7, %8, %9, %10, %7"
+                     : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),
+                       "+v"(r[6]), "+v"(r[7]), "=&s"(cc)
+                     : "v"(x), "v"(m));
+    } else if constexpr (OP == ADD_S) {
+        asm volatile("v_add_u32 %0, %9, %0\n\tv_add_u32 %1, %9, %1\n\tv_add_u32 %2, %9, %2\n\tv_add_u32 %3, %9, %3\n\tv_add_u32 %4, %9, %4\n\tv_add_u32 %5, %9, %5\n\tv_add_u32 %6, %9, %6\n\tv_add_u32 %7, %9, %7"
+                     : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
+                       "+v"(a[6]), "+v"(a[7])
+                     : "v"(x), "s"(m));
+    } else if constexpr (OP == ADD3_V) {
+        asm volatile("v_add3_u32 %0, %0, %8, %9\n\tv_add3_u32 %1, %1, %8, %9\n\tv_add3_u32 %2, %2, %8, %9\n\tv_add3_u32 %3, %3, %8, %9\n\tv_add3_u32 %4, %4, %8, %9\n\tv_add3_u32 %5, %5, %8, %9\n\tv_add3_u32 %6, %6, %8, %9\n\tv_add3_u32 %7, %7, %8, %9"
+                     : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
+                       "+v"(a[6]), "+v"(a[7])
+                     : "v"(x), "v"(m));
     } else if constexpr (OP == LSHL_OR) {
         asm volatile("v_lshl_or_b32 %0, %0, 3, %8\n\tv_lshl_or_b32 %1, %1, 3, %8\n\tv_lshl_or_b32 %2, %2, 3, %8\n\tv_lshl_or_b32 %3, %3, 3, %8\n\tv_lshl_or_b32 %4, %4, 3, %8\n\tv_lshl_or_b32 %5, %5, 3, %8\n\tv_lshl_or_b32 %6, %6, 3, %8\n\tv_lshl_or_b32 %7, %7, 3, %8"
                      : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
@@ -128,12 +151,24 @@ static void run(uint32_t W, uint32_t* d, unsigned long long* st) {
     (void)hipEventDestroy(e1);
 }
 
-int main() {
+int main(int argc, char** argv) {
+    const bool operands = argc > 1;  // "operands": SGPR vs VGPR operand variants only
     uint32_t* d;
     unsigned long long* st;
     (void)hipMalloc(&d, (size_t)256 * 8 * 256 * 4);
     (void)hipMalloc(&st, (size_t)256 * 8 * 2 * 8);
     for (uint32_t W : {1u, 2u, 8u}) {
+        if (operands) {
+            if (W == 1) continue;
+            run<XOR3>(W, d, st);
+            run<XOR3_V>(W, d, st);
+            run<MAD64>(W, d, st);
+            run<MAD64_V>(W, d, st);
+            run<ADD>(W, d, st);
+            run<ADD_S>(W, d, st);
+            run<ADD3_V>(W, d, st);
+            continue;
+        }
         run<XOR3>(W, d, st);
         run<ADD>(W, d, st);
         run<MAD64>(W, d, st);
