@@ -53,6 +53,7 @@ VALU_ISSUE_CYCLES = 2  # one wave64 VALU instruction per 2 cycles on a SIMD-32 (
 # code shape: v_mad_u64_u32 pairs + v_bitop3 xor3) by resident waves per SIMD
 PHILOX_PEAK_SRC = "profiles/r02_philox_bench.jsonl"
 PHILOX_PEAK_FALLBACK = {8: 9.69e11}
+PHILOX_BENCH_INSTS_PER_CALL = 40  # xor3 variant: 10 rounds x (2 v_mad_u64_u32 + 2 v_bitop3)
 # bytes one trial's own inputs and outputs occupy: faulty mask (u32) + order (u8)
 # read, decision word (u64) + outcome byte written (include/ba.h)
 IO_BYTES_IN, IO_BYTES_OUT = 5, 9
@@ -409,6 +410,13 @@ def main():
                         "peaks_by_waves_per_simd": {str(k): round(v / 1e9, 2) for k, v in sorted(peaks.items())},
                         "calls_per_launch": calls, "floor_ms": round(calls / peak * 1e3, 4),
                         "peak_source": PHILOX_PEAK_SRC}
+        if valu_roof:
+            # the kernel's VALU issue rate against the rate the Philox bench sustains at
+            # the same occupancy (its calls are 40 VOP3 instructions: 10 rounds x 2
+            # v_mad_u64_u32 + 2 v_bitop3), i.e. what this instruction mix can issue
+            bench_rate = peak * PHILOX_BENCH_INSTS_PER_CALL / 64
+            kern_rate = valu_roof["valu_insts_per_launch"] / (avg_ms * 1e-3)
+            compute_roof["valu_issue_rate_frac_of_philox_bench"] = round(kern_rate / bench_rate, 4)
         lsb = level_synchronous_bytes_per_trial(n, m) * B
         side = {"bytes_per_launch": lsb, "bytes_per_trial": lsb / B,
                 "equivalent_gbs": round(lsb / (avg_ms * 1e-3) / 1e9, 1),
