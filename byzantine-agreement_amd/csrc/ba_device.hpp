@@ -621,6 +621,7 @@ __device__ __forceinline__ uint32_t select_bit(uint32_t v, uint32_t j) {
 // (reference outputs: an address-taken local would live in scratch memory).
 __device__ __forceinline__ void gen_trial(uint32_t n, uint64_t seed, const GenSpec& g, uint64_t t,
                                           uint32_t& fmask, uint32_t& oc) {
+    if (g.faulty_mode == 0 && g.order_mode == 0) return;  // both given: no draw at all
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     P4 blk = philox10(P4{0u, kGenTag, (uint32_t)t, (uint32_t)(t >> 32)}, k0, k1);
     if (g.order_mode == 1) oc = blk.x >> 31;

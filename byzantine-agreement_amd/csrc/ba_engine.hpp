@@ -145,6 +145,12 @@ hipError_t launch_tail(const RunArgs& a, const Geometry& g, uint64_t W, const ui
                        const LevelsLayout& lay, const uint64_t* L1, const uint64_t* C2,
                        uint32_t c2base, uint64_t* decisions, uint8_t* outcome);
 
+// LEVELS big-batch root + quorum epilogue (ba_tail.hip, >= 64 groups of 64 words)
+bool epilogue_w_supported(const Geometry& g);
+hipError_t launch_epilogue_w(const RunArgs& a, const Geometry& g, uint64_t W,
+                             const uint64_t* scratch, const LevelsLayout& lay, const uint64_t* C1,
+                             uint64_t* decisions, uint8_t* outcome);
+
 hipError_t launch_table(const RunArgs& a, uint64_t* partials);
 hipError_t launch_gen_inputs(const RunArgs& a, uint32_t* faulty_out, uint8_t* order_out);
 hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_t* d_sender,

@@ -869,6 +869,11 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
     uint8_t* out = a.outcome ? a.outcome + trial0 : nullptr;
     static const bool old_epi = getenv("BA_EPILOGUE_PER_TRIAL") && atoi(getenv("BA_EPILOGUE_PER_TRIAL")) != 0;
     const uint64_t groups = (W + 63) / 64;
+    const bool no_epi_w = getenv("BA_NO_EPILOGUE_W") && atoi(getenv("BA_NO_EPILOGUE_W")) != 0;
+    if (!old_epi && !no_epi_w && epilogue_w_supported(g) && groups >= 64) {  // ba_tail.hip
+        ProfScope ps(a.prof, "k_epilogue", st);
+        return launch_epilogue_w(a, g, W, scratch, lay, C1, dec, out);
+    }
     if (!old_epi && g.n >= 4 && g.n <= 16 && g.me >= 1 && groups >= 64) {  // bit-sliced epilogue
         const uint32_t eb = (uint32_t)(groups < 4096 ? groups : 4096);
         const size_t lds = (size_t)(2 * g.L + 7 + g.n) * 64 * 8;
