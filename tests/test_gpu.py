@@ -468,20 +468,27 @@ def test_random_configs_fuzz(engine):
         assert {k: res.counters[k] for k in ocnt} == ocnt, tag
 
 
-@pytest.mark.parametrize("n,m", [(4, 1), (7, 2), (10, 3), (16, 2), (13, 1)])
-def test_levels_bitsliced_epilogue_vs_oracle(engine, n, m):
-    """LEVELS at a batch of >= 64 groups of 64 words takes the bit-sliced
-    epilogue (k_epilogue_bs): bit-exact with the oracle, given inputs including
-    non-attack/retreat ("other") orders and dense faulty sets, ragged tail."""
+@pytest.mark.parametrize("n,m", [(4, 1), (7, 2), (10, 3), (16, 2), (13, 1), (15, 3)])
+@pytest.mark.parametrize("epi_w", ["1", "0"])
+def test_levels_bitsliced_epilogue_vs_oracle(monkeypatch, n, m, epi_w):
+    """LEVELS at a batch of >= 64 groups of 64 words takes the big-batch epilogue
+    (k_epilogue_w; BA_NO_EPILOGUE_W=1: the previous k_epilogue_bs): bit-exact
+    with the oracle, given inputs including non-attack/retreat ("other") orders
+    and dense faulty sets, ragged tail."""
     from ba_amd import lib as L
+    monkeypatch.setenv("BA_NO_EPILOGUE_W", "0" if epi_w == "1" else "1")
+    engine = L.Engine(0)
     rng = np.random.default_rng(n * 7 + m)
     B = 64 * 64 * 64 + 37
     fm = rng.integers(0, 1 << n, B, dtype=np.uint64).astype(np.uint32)
     fm &= rng.integers(0, 1 << n, B, dtype=np.uint64).astype(np.uint32)
     oc = rng.choice([0, 1, 2], B, p=[0.45, 0.45, 0.1]).astype(np.uint8)
     od, oo, ocnt = oracle_c.run(n, m, B, seed=9, faulty=fm, order=oc, first_trial=64 * 3)
-    res = engine.run(n, m, B, seed=9, faulty=fm, order=oc, first_trial=64 * 3,
-                     engine=L.ENGINE_LEVELS)
+    try:
+        res = engine.run(n, m, B, seed=9, faulty=fm, order=oc, first_trial=64 * 3,
+                         engine=L.ENGINE_LEVELS)
+    finally:
+        engine.close()
     same(res.decisions, od, f"decisions n={n} m={m}")
     same(res.outcome, oo, f"outcome n={n} m={m}")
     assert {k: res.counters[k] for k in ocnt} == ocnt
