@@ -68,6 +68,50 @@ __global__ __launch_bounds__(kBlock) void k_input(uint32_t n, uint64_t seed, Gen
     }
 }
 
+// Given (staged) inputs: a wave slices kInGivenWPW words, every load of them in
+// flight before the first ballot (one wave per word waited one round trip each
+// and needed 4x the waves).
+constexpr uint32_t kInGivenWPW = 4;
+__global__ __launch_bounds__(kBlock) void k_input_given(uint32_t n, uint64_t ntrials,
+                                                        const uint32_t* __restrict__ faulty,
+                                                        const uint8_t* __restrict__ order,
+                                                        uint64_t* __restrict__ scratch, uint64_t W,
+                                                        uint64_t offF, uint64_t offOB, uint64_t offOO,
+                                                        uint64_t offVAL) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t base = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); base < W;
+         base += nwaves * kInGivenWPW) {
+        uint32_t fm[kInGivenWPW], oc[kInGivenWPW];
+#pragma unroll
+        for (uint32_t k = 0; k < kInGivenWPW; ++k) {
+            const uint64_t w = base + k * nwaves, i = w * 64 + lane;
+            const bool ok = w < W && i < ntrials;
+            fm[k] = ok ? faulty[i] : 0u;
+            oc[k] = ok ? order[i] : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kInGivenWPW; ++k) {
+            const uint64_t w = base + k * nwaves;
+            if (w >= W) break;
+            const bool valid = w * 64 + lane < ntrials;
+            uint64_t mine = 0;
+            for (uint32_t g = 0; g < n; ++g) {
+                const uint64_t b = __ballot(valid && ((fm[k] >> g) & 1u));
+                if (lane == g) mine = b;
+            }
+            const uint64_t ob = __ballot(valid && oc[k] == 1), oo = __ballot(valid && oc[k] == 2);
+            const uint64_t vv = __ballot(valid);
+            if (lane < n) scratch[offF + (uint64_t)lane * W + w] = mine;
+            if (lane == 0) {
+                scratch[offOB + w] = ob;
+                scratch[offOO + w] = oo;
+                scratch[offVAL + w] = vv;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // relay level k: one thread per (slot pair, word); one Philox call per thread.
 // Level k holds global slots [xbase, xbase + xcnt) (a first-hop subtree range;
@@ -724,7 +768,13 @@ hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_
     tin.offOO = lay.OO;
     tin.offVAL = lay.VAL;
     hipError_t e = hipSuccess;
-    if (!tin.fuse) {
+    if (!tin.fuse && given_in) {
+        ProfScope ps(a.prof, "k_input", st);
+        hipLaunchKernelGGL(k_input_given, dim3(blocks_for(W * 64 / kInGivenWPW, 4096)), dim3(kBlock), 0,
+                           st, a.n, ntrials, a.faulty + trial0, a.order + trial0, scratch, W, lay.F,
+                           lay.OB, lay.OO, lay.VAL);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    } else if (!tin.fuse) {
         ProfScope ps(a.prof, "k_input", st);
         hipLaunchKernelGGL(k_input, dim3(blocks_for(W * 64, 4096)), dim3(kBlock), 0, st, a.n, a.seed,
                            a.gen, a.first_trial + trial0, ntrials,
