@@ -112,6 +112,10 @@ def kernel_io_bytes(name: str, n: int, m: int, batch: int, staged: bool) -> int:
         return (IO_BYTES_IN if staged else 0) * batch + IO_BYTES_OUT * batch
     if name == "k_leaf":  # levels me-1, me never materialised: read L_{me-2}, write R_{me-1}
         return 8 * words * (S[me - 2] + S[me - 1])
+    if name == "k_leaf_up":  # read L_{me-2}, write R_{me-2} (the sibling-group majority)
+        return 8 * words * 2 * S[me - 2]
+    if name == "k_epilogue":  # read L_0, the level-1 votes and the n + 3 input planes; write I/O
+        return 8 * words * (S[0] + S[1] + n + 3) + IO_BYTES_OUT * batch
     if name == "k_relay_top":  # write levels 0..me-2 once
         return 8 * words * sum(S[: me - 1])
     return 0

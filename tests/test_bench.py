@@ -52,3 +52,11 @@ def test_cpu_threads_follows_omp(monkeypatch):
     assert bench.cpu_threads() == 3
     monkeypatch.delenv("OMP_NUM_THREADS")
     assert bench.cpu_threads() >= 1
+
+
+def test_kernel_io_bytes_levels():
+    W = (1 << 20) // 64
+    assert bench.kernel_io_bytes("k_leaf_up", 10, 3, 1 << 20, staged=True) == 8 * W * 2 * 72
+    assert bench.kernel_io_bytes("k_relay_top", 10, 3, 1 << 20, staged=True) == 8 * W * (9 + 72)
+    assert bench.kernel_io_bytes("k_epilogue", 10, 3, 1 << 20, staged=True) == \
+        8 * W * (9 + 72 + 13) + 9 * (1 << 20)
