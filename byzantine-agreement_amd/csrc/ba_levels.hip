@@ -5,9 +5,13 @@
 // 64 lanes of a wave touch 64 consecutive words of one slot (512 B, coalesced).
 //
 //   k_input     bit-slices per-trial inputs: F[g][w] = ballot(general g faulty)
+//               (k_input_given: staged inputs, four words per wave)
 //   k_relay     L_k[x] = F[sender] ? lie(x) : L_{k-1}[parent(x)]   (ba.py:42-57, 263-277)
+//   k_relay_top levels 0..K in one launch (ancestor chains)
 //   k_majority  R_p[sigma.r] = [2a > s] over L_p[sigma.r] and R_{p+1}[sigma.j.r] (ba.py:159-195)
 //   k_epilogue  root majority (tie -> undefined), quorum, IC flags    (ba.py:188-255)
+// The leaf-fused kernels (k_leaf, k_leaf_up) are in ba_fused.hip; the small-batch
+// tail (k_tail) and the big-batch epilogue (k_epilogue_w) in ba_tail.hip.
 #include "ba_engine.hpp"
 
 namespace ba {
