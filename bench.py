@@ -14,6 +14,15 @@ majority is resolved, every lieutenant's root decision is written to HBM
 the kernel too.  Both passes follow a common warm-up of >= 1 s of back-to-back
 steps, so neither pays the clock ramp.
 
+Steps in flight (--streams, default 2): step i is enqueued on stream i % 2, each
+stream with its own library ctx and output buffers, so two steps can run at
+once.  A WAVE launch's last ~quarter runs one wave per SIMD (the SIMD's older
+wave wins issue arbitration and finishes first); the next step's waves fill
+those slots.  Every step is still a complete 1M-trial pass; the counters of
+all K steps are checked against a one-stream pass of the same steps, reported
+as `value_single_stream`, whose per-step HIP-event time is also the kernel's
+launch time the roofline uses (and that rocprofv3 reports for --streams 1).
+
 N>1: launched one process per GPU by torch.distributed.run.  Trials shard by
 global index (weak scaling, no data-path collective); the run counters are
 all-reduced once over RCCL inside the C ABI (ba_comm_allreduce_device) at the
@@ -217,6 +226,9 @@ def main():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--inputs-in-kernel", action="store_true",
                     help="draw faulty sets/orders inside the timed kernel (no staging)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="steps in flight: step i runs on stream (and ctx) i %% streams, so the next "
+                         "step's waves fill the SIMDs a finishing step leaves idle")
     args = ap.parse_args()
 
     import torch
@@ -249,14 +261,21 @@ def main():
             print(f"bench: RCCL communicator failed ({e}); counters all-reduced over gloo",
                   file=sys.stderr, flush=True)
             collective = f"gloo fallback (RCCL failed: {e})"
-    dec = torch.empty(B, dtype=torch.int64, device=dev)
-    out = torch.empty(B, dtype=torch.uint8, device=dev)
+    NS = max(1, args.streams)
     cnt = torch.zeros(16, dtype=torch.int64, device=dev)
-    # a dedicated (non-null) stream: the library launches every kernel on it, so
-    # the HIP events below bracket exactly the hot-path kernels
-    stream = torch.cuda.Stream(dev)
+    # dedicated (non-null) streams, one library ctx each (a ctx orders its own calls,
+    # so steps overlap only across ctxs); every ctx adds its run counters into cnt
+    # (atomic sums).  Stream 0 carries the HIP events and the collectives.
+    # The steps run on the ctxs' own streams: ctxs created one after another get
+    # streams on different hardware queues (two torch pool streams can share one
+    # queue, which serialises them: rocprofv3 showed both on queue 4).
+    engines = [eng] + [L.Engine(dev.index) for _ in range(NS - 1)]
+    streams = [torch.cuda.ExternalStream(e.stream(), device=dev) for e in engines]
+    stream = streams[0]
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
+    decs = [torch.empty(B, dtype=torch.int64, device=dev) for _ in range(NS)]
+    outs = [torch.empty(B, dtype=torch.uint8, device=dev) for _ in range(NS)]
 
     def first_of(i):
         return (i * world + rank) * B  # global trial index: weak scaling, disjoint shards
@@ -279,16 +298,19 @@ def main():
             staged_params.append(L.make_params(n, m, args.seed, L.LIE_PHILOX, L.FAULTY_GIVEN, fmax,
                                                L.ORDER_GIVEN, L.ATTACK, engine_id, first_of(i)))
     torch.cuda.synchronize(dev)
-    dptr, optr, cptr = dec.data_ptr(), out.data_ptr(), cnt.data_ptr()
+    cptr = cnt.data_ptr()
 
-    def step(i, in_kernel):
+    def step(i, in_kernel, ns=NS):
+        j = i % ns
+        e, st = engines[j], streams[j].cuda_stream
+        dptr, optr = decs[j].data_ptr(), outs[j].data_ptr()
         if in_kernel:
-            eng.run_device(gen_params[i], B, d_decisions=dptr, d_outcome=optr, d_counters=cptr,
-                           stream=sp)
+            e.run_device(gen_params[i], B, d_decisions=dptr, d_outcome=optr, d_counters=cptr,
+                         stream=st)
         else:
             fp, op = staged[i]
-            eng.run_device(staged_params[i], B, d_faulty=fp, d_order=op, d_decisions=dptr,
-                           d_outcome=optr, d_counters=cptr, stream=sp)
+            e.run_device(staged_params[i], B, d_faulty=fp, d_order=op, d_decisions=dptr,
+                         d_outcome=optr, d_counters=cptr, stream=st)
 
     # common warm-up: >= warm_s of back-to-back steps (both modes) before any timing,
     # so the first timed pass does not pay the clock / power ramp
@@ -310,7 +332,7 @@ def main():
 
     bar = torch.zeros(16, dtype=torch.int64, device=dev)  # RCCL barrier operand
 
-    def timed(base, in_kernel):
+    def timed(base, in_kernel, ns=NS):
         cnt.zero_()
         torch.cuda.synchronize(dev)
         if dist:
@@ -322,8 +344,12 @@ def main():
         ev1 = torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record(stream)
+        for j in range(1, ns):
+            streams[j].wait_event(ev0)
         for i in range(args.steps):
-            step(base + i, in_kernel)
+            step(base + i, in_kernel, ns)
+        for j in range(1, ns):
+            stream.wait_stream(streams[j])
         ev1.record(stream)
         if comm is not None:
             # the only collective: the run counters (RCCL).  It is also the closing
@@ -353,6 +379,13 @@ def main():
         if counters2 != counters:
             raise SystemExit(f"staged-input and in-kernel-input runs disagree: {counters} vs {counters2}")
         value_gen = total_trials / T2
+    # the same steps one at a time on one stream: the single-stream rate, and (one launch
+    # per step) the kernel's own average launch time for the roofline below
+    T1, gpu_ms_1 = timed(base, args.inputs_in_kernel, 1)
+    counters1 = dict(zip(L.COUNTER_NAMES, [int(x) for x in cnt.cpu().tolist()]))
+    if counters1 != counters:
+        raise SystemExit(f"{NS}-stream and one-stream runs disagree: {counters} vs {counters1}")
+    value_1 = total_trials / T1
 
     # per-kernel HIP-event timing on the launch stream (a further pass of new steps)
     kernels, roof, valu_roof, compute_roof, side = {}, None, None, None, None
@@ -360,7 +393,7 @@ def main():
     if not args.no_profile:
         eng.profile(True)
         for i in range(args.steps):
-            step(base + args.steps + i, args.inputs_in_kernel)
+            step(base + args.steps + i, args.inputs_in_kernel, 1)
         torch.cuda.synchronize(dev)
         kernels = eng.profile_read()
         eng.profile(False)
@@ -371,10 +404,10 @@ def main():
         avg_src = "per-launch HIP events (profiling pass)"
         if len(kernels) == 1 and nl == args.steps:
             # a step is exactly one launch of this kernel: its average duration is the
-            # timed region's HIP-event time over the steps (the per-launch event pairs
-            # of the profiling pass add ~3 us of event overhead to each launch)
-            avg_ms = gpu_ms / args.steps
-            avg_src = "timed-region HIP events / steps (one launch per step)"
+            # one-stream timed region's HIP-event time over the steps (the per-launch
+            # event pairs of the profiling pass add ~3 us of event overhead to each)
+            avg_ms = gpu_ms_1 / args.steps
+            avg_src = "one-stream timed-region HIP events / steps (one launch per step)"
         digest = so_digest()
         pmc, pmc_src, same_build = pmc_for(n, m, B, args.engine, name, digest)
         io = kernel_io_bytes(name, n, m, B, staged_mode)
@@ -421,6 +454,24 @@ def main():
             bench_rate = peak * PHILOX_BENCH_INSTS_PER_CALL / 64
             kern_rate = valu_roof["valu_insts_per_launch"] / (avg_ms * 1e-3)
             compute_roof["valu_issue_rate_frac_of_philox_bench"] = round(kern_rate / bench_rate, 4)
+        if NS > 1 and len(kernels) == 1 and nl == args.steps:
+            # with NS steps in flight a launch spans ~NS x its one-stream time (rocprofv3
+            # reports that span), while the GPU completes one step per eff_ms: the
+            # throughput-side figures of the same kernel
+            eff_ms = gpu_ms / args.steps
+            roof["effective_ms_per_step"] = round(eff_ms, 4)
+            roof["achieved_effective"] = round(io / (eff_ms * 1e-3) / 1e9, 1)
+            roof["frac_effective"] = round(io / (eff_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            if valu_roof:
+                valu_roof["frac_effective"] = round(
+                    valu_roof["valu_insts_per_launch"] * VALU_ISSUE_CYCLES /
+                    (SIMDS * eff_ms * 1e-3 * CLOCK_GHZ * 1e9), 4)
+            wps_eff = min(NS * wps, max(peaks))
+            peak_eff = peaks.get(wps_eff, max(peaks.values()))
+            compute_roof["effective"] = {
+                "ms_per_step": round(eff_ms, 4), "achieved": round(calls / (eff_ms * 1e-3) / 1e9, 2),
+                "peak": round(peak_eff / 1e9, 2), "peak_waves_per_simd": wps_eff,
+                "frac": round(calls / (eff_ms * 1e-3) / peak_eff, 4)}
         lsb = level_synchronous_bytes_per_trial(n, m) * B
         side = {"bytes_per_launch": lsb, "bytes_per_trial": lsb / B,
                 "equivalent_gbs": round(lsb / (avg_ms * 1e-3) / 1e9, 1),
@@ -445,8 +496,14 @@ def main():
             "collective": collective,
             "inputs": "in-kernel Philox draws" if args.inputs_in_kernel else
                       "staged in HBM before the timed region (ba_gen_inputs_device); lies drawn in-kernel",
+            "schedule": (f"step i on stream/ctx i % {NS}: up to {NS} steps in flight, each a full "
+                         "1M-trial pass with its own outputs; every step's counters summed and checked"
+                         if NS > 1 else "one step at a time on one stream"),
             "ms_per_step_gpu_events": round(gpu_ms / args.steps, 4),
             "value_gpu_events": round(B * args.steps / (gpu_ms * 1e-3), 1),
+            "streams": NS,
+            "value_single_stream": round(value_1, 1),
+            "ms_per_step_single_stream_gpu_events": round(gpu_ms_1 / args.steps, 4),
             "value_with_input_generation": round(value_gen, 1) if value_gen else None,
             "ms_per_step_with_input_generation_gpu_events": round(gen_ms / args.steps, 4) if gen_ms else None,
             "warm_up_s": round(warm_s, 2),
@@ -463,7 +520,8 @@ def main():
         comm.close()
     if dist:
         dist.destroy_process_group()
-    eng.close()
+    for e in engines:
+        e.close()
 
 
 if __name__ == "__main__":

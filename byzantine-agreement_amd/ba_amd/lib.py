@@ -37,7 +37,7 @@ EXPORTS = ["ba_version", "ba_device_count", "ba_ctx_create", "ba_ctx_destroy", "
            "ba_engine_for", "ba_profile_enable", "ba_profile_read", "ba_mt_seed", "ba_mt_next32",
            "ba_om1_coin_count", "ba_mt_draw_coins", "ba_mt_table", "ba_vote_slots",
            "ba_subtree_votes_device", "ba_root_from_votes_device", "ba_gen_inputs_device",
-           "ba_ctx_device", "ba_comm_unique_id", "ba_comm_create", "ba_comm_destroy",
+           "ba_ctx_device", "ba_ctx_stream", "ba_comm_unique_id", "ba_comm_create", "ba_comm_destroy",
            "ba_trial_share", "ba_run_trials_multi", "ba_comm_rank", "ba_subtree_share",
            "ba_comm_allreduce_device", "ba_comm_allgather_votes_device",
            "ba_run_instance_split_multi", "ba_split_units", "ba_split_vote_slots",
@@ -126,6 +126,7 @@ def load(path: str | None = None):
     lib.ba_root_from_votes_device.argtypes = [vp, ctypes.POINTER(Params), u64, vp, vp, vp, vp, vp,
                                               vp, vp]
     lib.ba_ctx_device.argtypes = [vp, ctypes.POINTER(i32)]
+    lib.ba_ctx_stream.argtypes = [vp, ctypes.POINTER(vp)]
     lib.ba_comm_unique_id.argtypes = [ctypes.c_char_p]
     lib.ba_comm_create.argtypes = [vp, i32, i32, ctypes.c_char_p, ctypes.POINTER(vp)]
     lib.ba_comm_destroy.argtypes = [vp]
@@ -248,6 +249,12 @@ class Engine:
                                                 _ptr(order), _ptr(table), _ptr(poll), _ptr(dec),
                                                 _ptr(out), ctypes.byref(cnt)))
         return RunResult(dec, out, dict(zip(COUNTER_NAMES, [int(x) for x in cnt.v])))
+
+    def stream(self) -> int:
+        """The ctx's own HIP stream (ba_ctx_stream), as an int handle."""
+        h = ctypes.c_void_p()
+        _check(self.lib, self.lib.ba_ctx_stream(self.handle, ctypes.byref(h)))
+        return h.value or 0
 
     def profile(self, on: bool):
         """Enable/disable per-kernel HIP-event timing (clears the totals)."""

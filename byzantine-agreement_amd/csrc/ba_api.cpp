@@ -379,6 +379,12 @@ extern "C" int ba_ctx_device(ba_ctx* ctx, int* device) {
     return BA_OK;
 }
 
+extern "C" int ba_ctx_stream(ba_ctx* ctx, void** stream) {
+    if (!ctx || !stream) return fail(BA_EINVAL, "ctx and stream are required");
+    *stream = (void*)ctx->stream;
+    return BA_OK;
+}
+
 extern "C" void ba_ctx_destroy(ba_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);

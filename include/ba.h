@@ -253,6 +253,11 @@ int ba_root_from_split_votes_device(struct ba_ctx* ctx, const ba_params* p, uint
 #define BA_COMM_ID_BYTES 128
 struct ba_comm;
 int ba_ctx_device(struct ba_ctx* ctx, int* device);
+/* The ctx's own non-blocking HIP stream (the one ba_run_trials uses), valid as
+ * long as the ctx.  Callers without a HIP binding of their own (ctypes) can pass
+ * it to the *_device entry points; ctxs created one after another get streams
+ * on different hardware queues, so their calls can run concurrently. */
+int ba_ctx_stream(struct ba_ctx* ctx, void** stream);
 int ba_comm_unique_id(unsigned char id[BA_COMM_ID_BYTES]);
 int ba_comm_create(struct ba_ctx* ctx, int nranks, int rank,
                    const unsigned char id[BA_COMM_ID_BYTES], struct ba_comm** out);

@@ -154,6 +154,35 @@ def main():
                 _, sdt = timed(lambda: [call() for _ in range(reps_s)], world, dev)
                 res[B]["stream_seconds_per_call"] = sdt / reps_s
                 res[B]["stream_instances_per_s"] = B * reps_s / sdt
+                # two calls in flight: call i on ctx i % 2, each ctx on its own stream
+                # (ctx streams sit on different hardware queues) with its own outputs,
+                # so one call's short latency-bound launches overlap the other's leaf
+                # kernel; the counters of every call are summed and checked
+                eng2 = L.Engine(local)
+                ctxs = [(eng, eng.stream()), (eng2, eng2.stream())]
+                outs2 = [(torch.empty(B, dtype=torch.int64, device=dev),
+                          torch.empty(B, dtype=torch.uint8, device=dev)) for _ in ctxs]
+
+                def call2(i):
+                    e, s2 = ctxs[i % 2]
+                    d2, o2 = outs2[i % 2]
+                    e.run_device(pg, B, d_faulty=fb.data_ptr(), d_order=ob.data_ptr(),
+                                 d_decisions=d2.data_ptr(), d_outcome=o2.data_ptr(),
+                                 d_counters=sc.data_ptr(), stream=s2)
+                for i in range(4):  # warm-up of both ctxs
+                    call2(i)
+                torch.cuda.synchronize(dev)
+                sc.zero_()
+                torch.cuda.synchronize(dev)
+                _, s2dt = timed(lambda: [call2(i) for i in range(reps_s)], world, dev)
+                c2 = counters(sc)
+                if c2["trials"] != B * reps_s or any(v != counters(cnt)[k] * reps_s for k, v in c2.items()):
+                    raise SystemExit("config 5: two-stream calls' counters differ")
+                if not (torch.equal(outs2[0][0], dec) and torch.equal(outs2[1][1], o)):
+                    raise SystemExit("config 5: two-stream outputs differ from the split")
+                res[B]["stream2_seconds_per_call"] = s2dt / reps_s
+                res[B]["stream2_instances_per_s"] = B * reps_s / s2dt
+                eng2.close()
         out.append({"config": 5, "workload": f"OM({m}) n={n} (3,999,675 tree slots), "
                     f"{'first' if a.split_level == 1 else 'second'}-hop subtree split over "
                     f"{world} GPU(s), votes all-gathered", "split_level": a.split_level,
@@ -163,8 +192,10 @@ def main():
                     "throughput_instances_per_s_graph": res[a.batch5]["graph_instances_per_s"],
                     "latency_one_instance_ms_stream": res[1].get("stream_seconds_per_call", 0) * 1e3,
                     "throughput_instances_per_s_stream": res[a.batch5].get("stream_instances_per_s"),
-                    "stream_note": "staged inputs, calls launched back to back on one stream "
-                                   "(one rank only)",
+                    "latency_one_instance_ms_stream2": res[1].get("stream2_seconds_per_call", 0) * 1e3,
+                    "throughput_instances_per_s_stream2": res[a.batch5].get("stream2_instances_per_s"),
+                    "stream_note": "staged inputs, calls launched back to back on one stream; "
+                                   "stream2: two calls in flight on two ctx streams (one rank only)",
                     "n_gpus": world, "counters_batch": res[a.batch5]["counters"]})
 
     if rank == 0:
