@@ -561,3 +561,38 @@ def test_levels_small_batch_fusions_vs_oracle(monkeypatch, n, m, B):
             assert {k: res.counters[k] for k in gcnt} == gcnt
         finally:
             e.close()
+
+
+def test_two_ctxs_in_flight_equal_one_stream():
+    """bench.py's schedule: calls alternate over two ctxs, each on its own ctx stream
+    (ba_ctx_stream), so two run at once; every call's outputs and the summed counters
+    equal the same calls made one at a time, and equal the oracle."""
+    import torch
+    from ba_amd import lib as L
+    n, m, B, K = 10, 3, 64 * 257 + 5, 6
+    engs = [L.Engine(0), L.Engine(0)]
+    try:
+        sts = [e.stream() for e in engs]
+        assert sts[0] and sts[1] and sts[0] != sts[1]
+        cnt = torch.zeros(16, dtype=torch.int64, device="cuda")
+        decs = [torch.empty(B, dtype=torch.int64, device="cuda") for _ in range(K)]
+        outs = [torch.empty(B, dtype=torch.uint8, device="cuda") for _ in range(K)]
+        for i in range(K):
+            p = L.make_params(n, m, 0xBA5EED, L.LIE_PHILOX, L.FAULTY_RANDOM, 3, L.ORDER_RANDOM,
+                              L.ATTACK, L.ENGINE_AUTO, i * 64 * 300)
+            engs[i % 2].run_device(p, B, d_decisions=decs[i].data_ptr(), d_outcome=outs[i].data_ptr(),
+                                   d_counters=cnt.data_ptr(), stream=sts[i % 2])
+        torch.cuda.synchronize()
+        total = {k: 0 for k in L.COUNTER_NAMES}
+        for i in range(K):
+            od, oo, oc = oracle_c.run(n, m, B, seed=0xBA5EED, faulty_mode=L.FAULTY_RANDOM, f=3,
+                                      order_mode=L.ORDER_RANDOM, first_trial=i * 64 * 300)
+            same(decs[i].cpu().numpy().view(np.uint64), od, f"decisions call {i}")
+            same(outs[i].cpu().numpy(), oo, f"outcome call {i}")
+            for k, v in oc.items():
+                total[k] += v
+        got = dict(zip(L.COUNTER_NAMES, [int(x) for x in cnt.cpu().tolist()]))
+        assert {k: got[k] for k in total} == total
+    finally:
+        for e in engs:
+            e.close()

@@ -2,7 +2,9 @@
 # GPU-box session: every GPU step has its own time limit; a fault, abort or
 # timeout ends the session (no retries).  Logs land in gpurun_out/.
 # usage: tools/gpu_session.sh [stage ...]
-#   tests smoke bench bench_levels bench_fused prof pmc philox configs
+#   tests smoke bench bench_levels bench_fused prof prof1 pmc philox configs
+#   (prof: the default bench command, two steps in flight, so each k_om3w launch
+#   spans ~2x its own time; prof1: --streams 1, the launch time the roofline uses)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -18,7 +20,7 @@ run() {  # name seconds cmd...
   return $rc
 }
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }  # 1 = ordinary test failure
-BENCH_PMC="$ROOT/bench.py --steps 3 --warmup 1 --warm-s 0 --no-cpu --no-profile"
+BENCH_PMC="$ROOT/bench.py --steps 3 --warmup 1 --warm-s 0 --no-cpu --no-profile --streams 1"
 pmc_pass() {  # name counters...
   local name=$1; shift
   (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv \
@@ -38,6 +40,10 @@ for s in $STAGES; do
            timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/prof" -o run -- \
              python3 "$ROOT/bench.py" --steps 10 --warmup 2 --warm-s 0.3 --no-cpu --no-profile > "$ROOT/gpurun_out/prof.log" 2>&1); rc=$?
           echo "prof rc=$rc" | tee -a gpurun_out/steps.log; tail -3 gpurun_out/prof.log; [ $rc -eq 0 ] || exit $rc ;;
+    prof1) (cd /tmp && export TMPDIR=/tmp && mkdir -p "$ROOT/gpurun_out/prof1" && \
+           timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/prof1" -o run -- \
+             python3 "$ROOT/bench.py" --steps 10 --warmup 2 --warm-s 0.3 --no-cpu --no-profile --streams 1 > "$ROOT/gpurun_out/prof1.log" 2>&1); rc=$?
+          echo "prof1 rc=$rc" | tee -a gpurun_out/steps.log; tail -3 gpurun_out/prof1.log; [ $rc -eq 0 ] || exit $rc ;;
     pmc) pmc_pass sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY || exit $?
          pmc_pass fetch FETCH_SIZE GRBM_GUI_ACTIVE GRBM_COUNT || exit $?
          pmc_pass write WRITE_SIZE || exit $?
