@@ -421,9 +421,11 @@ def main():
                 "algorithmic_bytes_per_launch": io,
                 "algorithmic_bytes_per_trial": io / B,
                 "traffic_source": pmc_src, "traffic_same_build": same_build,
-                "note": "bytes the kernel must move: per-trial inputs (5 B, staged) and outputs "
-                        "(9 B); the OM tree lives in LDS/registers, so HBM is not this kernel's "
-                        "bound -- valu_roofline is"}
+                "note": ("bytes the kernel must move: per-trial inputs (5 B, staged) and outputs "
+                         "(9 B); the OM tree lives in LDS/registers, so HBM is not this kernel's "
+                         "bound -- valu_roofline is") if name.startswith(("k_om", "k_fused")) else
+                        ("bytes the kernel must move through the LEVELS arrays (kernel_io_bytes); "
+                         "it draws its leaf levels from Philox in registers, so it is VALU-bound")}
         if pmc and pmc.get("counters", {}).get("SQ_INSTS_VALU"):
             insts = pmc["counters"]["SQ_INSTS_VALU"]
             cycles = avg_ms * 1e-3 * CLOCK_GHZ * 1e9
