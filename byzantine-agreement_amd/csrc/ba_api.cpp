@@ -361,7 +361,8 @@ extern "C" int ba_ctx_create(int device, ba_ctx** out) {
         delete ctx;
         return fail(BA_EDEVICE, "hipStreamCreate/hipEventCreate: %s", hipGetErrorString(e));
     }
-    if (ctx->sink.grow(kSinkBytes) != BA_OK || hipMemset(ctx->sink.p, 0, kSinkBytes) != hipSuccess ||
+    if (ctx->sink.grow(kSinkBytes + kSinkTaskCounterBytes) != BA_OK ||
+        hipMemset(ctx->sink.p, 0, kSinkBytes + kSinkTaskCounterBytes) != hipSuccess ||
         hipDeviceSynchronize() != hipSuccess) {
         (void)hipStreamDestroy(ctx->stream);
         (void)hipEventDestroy(ctx->last_ev);
@@ -534,6 +535,7 @@ static RunArgs make_args(ba_ctx* ctx, const ba_params* p, uint64_t batch, const 
     a.prof = &ctx->prof;
     a.cu_count = ctx->cu_count;
     a.sink.rep = (unsigned long long*)ctx->sink.p;
+    a.sink.tasks = (unsigned int*)((char*)ctx->sink.p + kSinkBytes);
     return a;
 }
 

@@ -496,7 +496,11 @@ constexpr unsigned long long kSinkValueMask = (1ull << kSinkArrivalShift) - 1;
 
 struct Sink {
     unsigned long long* rep;  // [kSinkReplicas][kSinkRepStride], zero between launches
+    // WAVE engines' dynamic task counter (ctx-owned, zeroed by the launch's stream
+    // right before a persistent launch; nullptr = static task assignment)
+    unsigned int* tasks = nullptr;
 };
+constexpr size_t kSinkTaskCounterBytes = 64;  // after the replicas, a line of its own
 
 // Called by every lane of one wave; lane c < C_NUM passes the unit's total of
 // counter c in v (other lanes: ignored).

@@ -687,6 +687,9 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
 #ifdef BA_FUSED_STAMPS
     const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
+    // static task stride: the bench's 1M-trial launch has one task per wave, and
+    // the dynamic counter of k_om4w cost this kernel 6 VGPRs (163 -> 169: no
+    // third wave per SIMD for a second launch in flight)
     for (uint64_t task = (uint64_t)blockIdx.x * wpb + wv; task < ntasks;
          task += (uint64_t)gridDim.x * wpb) {
         const uint64_t w0 = task * W;
@@ -1142,8 +1145,16 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om4w(
     const bool act = lane < (uint32_t)G::LANES;
     const uint32_t lw = act ? lw_ : 0;
     TrialCounts tc;
-    for (uint64_t task = (uint64_t)blockIdx.x * wpb + wv; task < ntasks;
-         task += (uint64_t)gridDim.x * wpb) {
+    // tasks: the first wave-round static, then (sk.tasks != nullptr: a persistent
+    // launch) each further task from the launch's atomic counter, fetched at the
+    // start of the current task so its latency hides behind the task: a wave
+    // that issues faster (a SIMD's older wave wins arbitration) takes more
+    // tasks, instead of finishing its fixed share early and leaving its SIMD to
+    // one wave for the rest of the launch
+    const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
+    for (uint64_t task = (uint64_t)blockIdx.x * wpb + wv; task < ntasks;) {
+        uint32_t next_raw = 0;
+        if (sk.tasks != nullptr && lane == 0) next_raw = atomicAdd(sk.tasks, 1u);
         const uint64_t w0 = task * W;
         const uint64_t gw0 = (first_trial >> 6) + w0;
         wave_inputs<N, W, 0>(img + G::oIN, lane, w0, seed, gs, first_trial, batch, faulty, order);
@@ -1245,6 +1256,7 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om4w(
         __builtin_amdgcn_wave_barrier();
         wave_epilogue<N, W, ME, 0>(img + G::oIN, img + G::oAU, lane, w0, batch, decisions, outcome, tc);
         __builtin_amdgcn_wave_barrier();
+        task = sk.tasks != nullptr ? nwaves + __builtin_amdgcn_readfirstlane(next_raw) : task + nwaves;
     }
     wave_flush(tc, lane, wv, wpb, counters, sk, false);
 }
@@ -1254,7 +1266,8 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om4w(
 // and a persistent task loop.  `staged` (optional) replaces `kernel` when both
 // inputs are given.
 template <typename G, typename K>
-inline hipError_t launch_wave(const RunArgs& a, K kernel, const char* name, K staged = nullptr) {
+inline hipError_t launch_wave(const RunArgs& a, K kernel, const char* name, K staged = nullptr,
+                              bool dyn_tasks = false) {
     if (staged && a.gen.faulty_mode == 0 && a.gen.order_mode == 0) kernel = staged;
     constexpr uint32_t wpb = kWaveThreads / 64;
     const uint64_t words = (a.batch + 63) / 64, tasks = (words + G::W - 1) / G::W;
@@ -1265,10 +1278,21 @@ inline hipError_t launch_wave(const RunArgs& a, K kernel, const char* name, K st
         if (c >= 1 && c < cap) cap = c;
     }
     if (blocks > cap) blocks = cap;
+    // persistent launch (more tasks than waves) of a kernel with the dynamic loop
+    // (k_om4w): task assignment from the ctx's counter, zeroed on the launch's
+    // stream (BA_WAVE_STATIC_TASKS=1: the static stride loop, A/B only)
+    Sink sk = a.sink;
+    const bool stat = getenv("BA_WAVE_STATIC_TASKS") && atoi(getenv("BA_WAVE_STATIC_TASKS")) != 0;
+    if (!dyn_tasks || stat || tasks <= blocks * wpb || sk.tasks == nullptr) {
+        sk.tasks = nullptr;
+    } else {
+        const hipError_t e = hipMemsetAsync(sk.tasks, 0, sizeof(unsigned int), a.stream);
+        if (e != hipSuccess) return e;
+    }
     ProfScope ps(a.prof, name, a.stream);
     hipLaunchKernelGGL(kernel, dim3((uint32_t)blocks), dim3(kWaveThreads), wpb * G::words * 8,
                        a.stream, a.seed, a.gen, a.first_trial, a.batch, a.faulty, a.order,
-                       a.decisions, a.outcome, a.counters, a.sink);
+                       a.decisions, a.outcome, a.counters, sk);
     return hipGetLastError();
 }
 
