@@ -402,7 +402,9 @@ OM4_CASES = [(6, 4, 1), (6, 5, 2), (7, 4, 2), (8, 4, 2), (9, 4, 3), (10, 4, 3), 
 def test_om4_wave_vs_oracle(monkeypatch, n, m, f):
     """k_om4w (rounds over second-level subtrees, R1 counters per first hop)
     against the oracle on a ragged batch, with and without the persistent task
-    loop (BA_WAVE_MAX_BLOCKS=1), random faulty sets and given inputs."""
+    loop (BA_WAVE_MAX_BLOCKS=1 or 2: one or two blocks take tasks from the ctx's
+    dynamic counter; BA_WAVE_STATIC_TASKS=1: the static stride), random faulty
+    sets and given inputs."""
     from ba_amd import lib as L
     assert L.load().ba_engine_for(n, m) == L.ENGINE_FUSED
     B = 64 * 13 + 37
@@ -414,7 +416,8 @@ def test_om4_wave_vs_oracle(monkeypatch, n, m, f):
           ).astype(np.uint32)
     oc = rng.choice([0, 1, 2], B).astype(np.uint8)
     gd, go, gcnt = oracle_c.run(n, m, B, seed=3, faulty=fm, order=oc)
-    for cap in (None, "1"):
+    for cap, stat in ((None, "0"), ("1", "0"), ("2", "0"), ("2", "1")):
+        monkeypatch.setenv("BA_WAVE_STATIC_TASKS", stat)
         if cap:
             monkeypatch.setenv("BA_WAVE_MAX_BLOCKS", cap)
         else:
@@ -425,7 +428,7 @@ def test_om4_wave_vs_oracle(monkeypatch, n, m, f):
             given = e.run(n, m, B, seed=3, faulty=fm, order=oc, engine=L.ENGINE_FUSED)
         finally:
             e.close()
-        tag = f"n={n} m={m} cap={cap}"
+        tag = f"n={n} m={m} cap={cap} static={stat}"
         same(res.decisions, od, "decisions " + tag)
         same(res.outcome, oo, "outcome " + tag)
         assert {k: res.counters[k] for k in ocnt} == ocnt, tag
