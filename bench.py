@@ -250,7 +250,11 @@ def main():
     n, m, B = args.n, args.m, args.batch
     fmax = L.default_fmax(n) if args.fmax < 0 else args.fmax
     engine_id = {"auto": L.ENGINE_AUTO, "fused": L.ENGINE_FUSED, "levels": L.ENGINE_LEVELS}[args.engine]
-    eng = L.Engine(dev.index)
+    NS = max(1, args.streams)
+    # the steps' ctxs, created one after another before anything else makes streams
+    # (RCCL does): consecutive ctx streams land on different hardware queues
+    engines = [L.Engine(dev.index) for _ in range(NS)]
+    eng = engines[0]
     collective = None
     if world > 1:
         from ba_amd import dist as D
@@ -261,7 +265,6 @@ def main():
             print(f"bench: RCCL communicator failed ({e}); counters all-reduced over gloo",
                   file=sys.stderr, flush=True)
             collective = f"gloo fallback (RCCL failed: {e})"
-    NS = max(1, args.streams)
     cnt = torch.zeros(16, dtype=torch.int64, device=dev)
     # dedicated (non-null) streams, one library ctx each (a ctx orders its own calls,
     # so steps overlap only across ctxs); every ctx adds its run counters into cnt
@@ -269,7 +272,6 @@ def main():
     # The steps run on the ctxs' own streams: ctxs created one after another get
     # streams on different hardware queues (two torch pool streams can share one
     # queue, which serialises them: rocprofv3 showed both on queue 4).
-    engines = [eng] + [L.Engine(dev.index) for _ in range(NS - 1)]
     streams = [torch.cuda.ExternalStream(e.stream(), device=dev) for e in engines]
     stream = streams[0]
     torch.cuda.set_stream(stream)
