@@ -173,28 +173,46 @@ def cpu_threads() -> int:
         return os.cpu_count() or 1
 
 
-def run_cpu_baseline(n, m, seed, fmax, budget_s):
+def run_cpu_baseline(n, m, seed, fmax, budget_s, first, count, gpu_counters):
     """Time the word-sliced OpenMP C port (oracle/ba_sliced.c: 64 trials per word,
     one Philox call per two slot-words, the GPU engines' minimum draw count) on a
-    bounded sample of the same workload, inputs staged first as on the GPU."""
+    bounded sample of the same workload, inputs staged first as on the GPU.
+
+    The sample starts with exactly the trials of the GPU's timed steps,
+    [first, first + count): the port's run counters over them must equal the
+    GPU's (the quorum / IC tallies of ba.py:197-255), else the
+    bench exits non-zero.  It then continues with the next trials of the same
+    stream until ~budget_s of CPU work; `value` is all sampled trials over the
+    time of both runs."""
     import oracle_c
     threads = cpu_threads()
     kw = dict(seed=seed, faulty_mode=1, f=fmax, order_mode=1)
-    probe = 64 * 64 * threads
-    fm, oc = oracle_c.sliced_gen(n, probe, threads=threads, **kw)
-    t0 = time.perf_counter()
-    oracle_c.sliced_run(n, m, probe, seed=seed, faulty=fm, order=oc, threads=threads)
-    rate = probe / max(time.perf_counter() - t0, 1e-9)
-    sample = int(min(max(rate * budget_s, probe), 1 << 27)) // 64 * 64
-    fm, oc = oracle_c.sliced_gen(n, sample, threads=threads, **kw)
-    t0 = time.perf_counter()
-    _, _, c = oracle_c.sliced_run(n, m, sample, seed=seed, faulty=fm, order=oc, threads=threads)
-    dt = time.perf_counter() - t0
+
+    def timed_run(f0, cnt):
+        fm, oc = oracle_c.sliced_gen(n, cnt, threads=threads, first_trial=f0, **kw)
+        t0 = time.perf_counter()
+        _, _, c = oracle_c.sliced_run(n, m, cnt, seed=seed, faulty=fm, order=oc, first_trial=f0,
+                                      threads=threads, want_outputs=False)
+        return c, time.perf_counter() - t0
+
+    c_gpu_range, dt0 = timed_run(first, count)
+    want = {k: gpu_counters[k] for k in c_gpu_range}
+    match = c_gpu_range == want
+    if not match:
+        raise SystemExit(f"cpu_baseline: the C port's counters over the GPU's timed trials "
+                         f"[{first}, {first + count}) differ from the GPU's: {c_gpu_range} vs {want}")
+    rate = count / max(dt0, 1e-9)
+    extra = int(min(max(rate * budget_s - count, 0), 1 << 27)) // 64 * 64
+    dt1 = 0.0
+    if extra:
+        _, dt1 = timed_run(first + count, extra)
+    sample, dt = count + extra, dt0 + dt1
     value = sample / dt
     nproc = os.cpu_count() or 1
     return {"value": round(value, 1), "unit": "trial-decisions/s", "cores": threads, "kind": "port",
-            "sample": f"word-sliced OpenMP C port (oracle/ba_sliced.c, x{threads} threads) on the "
-                      f"first {sample} trials of the same n={n}, m={m} synthetic stream (inputs "
+            "sample": f"word-sliced OpenMP C port (oracle/ba_sliced.c, x{threads} threads) on "
+                      f"trials [{first}, {first + sample}) of the same n={n}, m={m} synthetic "
+                      f"stream: the GPU's {count} timed trials, then {extra} more (inputs "
                       f"staged first, as on the GPU), {dt:.1f} s; host CPU: {cpu_model()}, "
                       f"nproc={nproc}; {threads} threads = this job's CPU share "
                       f"(OMP_NUM_THREADS / affinity)",
@@ -202,10 +220,50 @@ def run_cpu_baseline(n, m, seed, fmax, budget_s):
             "all_cores_projection": {"value": round(value / threads * nproc, 1), "cores": nproc,
                                      "note": "per-thread rate x nproc, not measured (the pool "
                                              "grants this job its CPU share only)"},
-            "counters_trials": c["trials"],
+            "counters_match": match,
+            "counters_checked": {"first_trial": first, "trials": count,
+                                 "what": "all 12 run counters of the GPU's timed steps"},
             "reference_ba_py": {"value_us_per_trial": 574.0, "config": "OM(1) n=10, one core",
                                 "where": "dev container (Intel Xeon), BASELINE.md; ba.py cannot "
                                          "run on the GPU box (rpyc and the reference are absent)"}}
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_cmd(gpus: int, argv: list, port: int) -> list:
+    """The torch.distributed.run command bench.py starts for --gpus N > 1 when it
+    was not launched by one: N local ranks, rendezvous on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+            os.path.abspath(__file__)] + list(argv)
+
+
+def check_or_launch_world(gpus: int, argv: list, env) -> int | None:
+    """None: run this process as a rank (or alone).  Otherwise the exit code to
+    leave with: the launched job's, or 2 when a launcher's WORLD_SIZE disagrees
+    with --gpus (the line would report a different n_gpus than asked)."""
+    if gpus < 1:
+        print(f"bench: --gpus {gpus} must be >= 1", file=sys.stderr, flush=True)
+        return 2
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            print(f"bench: WORLD_SIZE={ws} but --gpus {gpus}: launch one rank per GPU asked for",
+                  file=sys.stderr, flush=True)
+            return 2
+        return None
+    if gpus == 1:
+        return None
+    import subprocess
+    cmd = launch_cmd(gpus, argv, free_port())
+    child_env = dict(env)
+    child_env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=child_env)
 
 
 def main():
@@ -230,6 +288,14 @@ def main():
                     help="steps in flight: step i runs on stream (and ctx) i %% streams, so the next "
                          "step's waves fill the SIMDs a finishing step leaves idle")
     args = ap.parse_args()
+
+    # --gpus N: one process per GPU.  Launched without a launcher (no WORLD_SIZE),
+    # N > 1 starts torch.distributed.run on N local ranks as a CHILD process and
+    # exits with its code; nothing here has touched the GPU yet.  Under a launcher
+    # the world it made must be the one asked for.
+    rc = check_or_launch_world(args.gpus, sys.argv[1:], os.environ)
+    if rc is not None:
+        raise SystemExit(rc)
 
     import torch
     from ba_amd import lib as L
@@ -484,7 +550,9 @@ def main():
                         "comparison figure only"}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = run_cpu_baseline(n, m, args.seed, fmax, args.cpu_budget_s)
+        # the GPU's timed steps at world 1: trials [base*B, (base+K)*B), contiguous
+        cpu = run_cpu_baseline(n, m, args.seed, fmax, args.cpu_budget_s, first_of(base),
+                               B * args.steps, counters)
 
     if rank == 0:
         line = {

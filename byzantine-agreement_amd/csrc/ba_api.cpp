@@ -724,8 +724,11 @@ static int ordered(ba_ctx* ctx, void* stream, F&& body) {
     const hipStream_t s = (hipStream_t)stream;
     HIP_TRY(hipSetDevice(ctx->device));
     HIP_TRY(ctx_order(ctx, s));
+    // marked whatever body() returned: a call that fails part-way may already
+    // have queued work on s that uses the ctx's scratch, sink or task counter,
+    // and the ctx's next call on another stream must wait for it
     const int rc = body();
-    if (rc == BA_OK) HIP_TRY(ctx_mark(ctx, s));
+    (void)ctx_mark(ctx, s);
     return rc;
 }
 

@@ -676,7 +676,12 @@ __global__ __launch_bounds__(kReduceThreads) void k_reduce(const uint64_t* __res
         if (t < stride) red[t] += red[t + stride];
         __syncthreads();
     }
-    if (t < 16) counters[t] += red[t];
+    // atomic adds: two table-mode calls in flight on two ctx streams may share
+    // one counter array, like the sink of the other engines
+    if (t < 16)
+        __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(counters) + t,
+                               (unsigned long long)red[t], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------

@@ -32,6 +32,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/ba.h"
@@ -287,6 +288,42 @@ static int finish_job(ba_comm* comm, int local_rc, ba_counters* counters_out, bo
     return BA_OK;
 }
 
+// BA_FORCE_SPLIT=1: the split entry takes the vote-array path at one rank
+// (test-only; read on every call, so a test can switch it in-process).
+static bool force_split() {
+    const char* e = getenv("BA_FORCE_SPLIT");
+    return e && e[0] == '1';
+}
+
+// Sum every rank's error flag now, synchronously, before a collective that a
+// failed rank could not join.  Returns BA_OK when no rank failed; otherwise
+// this rank's own error, or "another rank failed" -- the same answer on every
+// rank, so all of them leave the call together.  The error slot is left at 0
+// for finish_job when no rank failed.
+static int preagree(ba_comm* comm, int local_rc) {
+    const uint64_t flag = local_rc != BA_OK ? 1 : 0;
+    uint64_t got = 0;
+    int rc = BA_OK;
+    Rccl& r = rccl();
+    if (hipMemcpyAsync(comm->d_cnt + kErrSlot, &flag, sizeof flag, hipMemcpyHostToDevice,
+                       comm->stream) != hipSuccess)
+        rc = failf(BA_EDEVICE, "error-flag upload");
+    const ncclResult_t e = r.all_reduce(comm->d_cnt + kErrSlot, comm->d_cnt + kErrSlot, 1, ncclUint64,
+                                        ncclSum, comm->comm, comm->stream);
+    if (e != ncclSuccess && rc == BA_OK) rc = failf(BA_EDEVICE, "ncclAllReduce: %s", r.error_string(e));
+    if ((hipMemcpyAsync(&got, comm->d_cnt + kErrSlot, sizeof got, hipMemcpyDeviceToHost,
+                        comm->stream) != hipSuccess ||
+         hipStreamSynchronize(comm->stream) != hipSuccess) &&
+        rc == BA_OK)
+        rc = failf(BA_EDEVICE, "error-flag read-back");
+    if (local_rc != BA_OK) return local_rc;
+    if (rc != BA_OK) return rc;
+    if (got != 0)
+        return failf(BA_EDEVICE, "%llu other rank(s) failed this call before the vote exchange",
+                     (unsigned long long)got);
+    return BA_OK;
+}
+
 static int begin_job(ba_comm* comm) {
     if (hipSetDevice(comm->device) != hipSuccess) return failf(BA_EDEVICE, "hipSetDevice");
     if (hipMemsetAsync(comm->d_cnt, 0, BA_NCOUNTERS * sizeof(uint64_t), comm->stream) != hipSuccess)
@@ -337,7 +374,11 @@ extern "C" int ba_run_instance_split_level_multi(struct ba_ctx* ctx, struct ba_c
                     ? failf(BA_ENOTSUP, "no level-%u split for n=%u, m=%u (OM(0) has no relay "
                             "subtrees; the second-hop split needs m_eff >= 3)", level, n, p->m)
                     : failf(BA_EINVAL, "split level %u (1: first hop, 2: second hop)", level);
-    if (comm->nranks == 1) {  // one rank owns every unit: the unsplit pass, no vote array
+    // one rank owns every unit: the unsplit pass, no vote array -- unless
+    // BA_FORCE_SPLIT=1 (test-only switch), which runs the vote array, the
+    // grouped-broadcast exchange and the agreement steps on a one-rank
+    // communicator, so the real RCCL code runs on a one-GPU box
+    if (comm->nranks == 1 && !force_split()) {
         if (local == BA_OK && batch > 0)
             local = ba_run_trials_device(ctx, p, batch, d_faulty_mask, d_order, nullptr, nullptr,
                                          d_decisions, d_outcome, comm->d_cnt, comm->stream);
@@ -350,10 +391,19 @@ extern "C" int ba_run_instance_split_level_multi(struct ba_ctx* ctx, struct ba_c
         if (comm->d_votes) (void)hipFree(comm->d_votes);
         comm->d_votes = nullptr;
         comm->votes_bytes = 0;
-        if (hipMalloc(&comm->d_votes, need) != hipSuccess)
+        const char* inj = getenv("BA_TEST_VOTE_ENOMEM");  // test-only: inject the failure
+        if ((inj && inj[0] == '1') || hipMalloc(&comm->d_votes, need) != hipSuccess)
             local = failf(BA_ENOMEM, "vote buffer (%zu B)", need);
         else
             comm->votes_bytes = need;
+    }
+    // Agree before the exchange: a rank that failed validation or could not
+    // allocate its vote buffer cannot join the grouped broadcasts (its peers
+    // would wait in them forever), so every rank learns of any failure here
+    // and all of them skip the exchange together.
+    {
+        const int rc_pre = preagree(comm, local);
+        if (rc_pre != BA_OK) return rc_pre;
     }
     if (local == BA_OK && batch > 0) {
         uint32_t ub = 0, ue = 0;

@@ -145,13 +145,18 @@ __device__ __forceinline__ void gen_words(uint64_t* in0, uint32_t lane, uint64_t
 // data SGPR early: without wait states between them a GPU run got wrong planes
 // (the hazard recognizer cannot see into the asm), so each group of up to 4
 // planes pays one s_nop 4 after its ballots.
+// BA_WRITELANE_NOP: the wait states in front of each group (tests/test_lib.py
+// builds a copy with it empty to prove its code-object check catches that).
+#ifndef BA_WRITELANE_NOP
+#define BA_WRITELANE_NOP "s_nop 4\n\t"
+#endif
 template <int G0, int CNT>
 __device__ __forceinline__ void writelane4(uint32_t& lo, uint32_t& hi, const uint64_t (&b)[4]) {
     const uint32_t l0 = (uint32_t)b[0], h0 = (uint32_t)(b[0] >> 32), l1 = (uint32_t)b[1],
                    h1 = (uint32_t)(b[1] >> 32), l2 = (uint32_t)b[2], h2 = (uint32_t)(b[2] >> 32),
                    l3 = (uint32_t)b[3], h3 = (uint32_t)(b[3] >> 32);
     if constexpr (CNT == 4)
-        asm volatile("s_nop 4\n\tv_writelane_b32 %0, %2, %10\n\tv_writelane_b32 %1, %3, %10\n\t"
+        asm volatile(BA_WRITELANE_NOP "v_writelane_b32 %0, %2, %10\n\tv_writelane_b32 %1, %3, %10\n\t"
                      "v_writelane_b32 %0, %4, %11\n\tv_writelane_b32 %1, %5, %11\n\t"
                      "v_writelane_b32 %0, %6, %12\n\tv_writelane_b32 %1, %7, %12\n\t"
                      "v_writelane_b32 %0, %8, %13\n\tv_writelane_b32 %1, %9, %13"
@@ -159,19 +164,19 @@ __device__ __forceinline__ void writelane4(uint32_t& lo, uint32_t& hi, const uin
                      : "s"(l0), "s"(h0), "s"(l1), "s"(h1), "s"(l2), "s"(h2), "s"(l3), "s"(h3),
                        "i"(G0), "i"(G0 + 1), "i"(G0 + 2), "i"(G0 + 3));
     else if constexpr (CNT == 3)
-        asm volatile("s_nop 4\n\tv_writelane_b32 %0, %2, %8\n\tv_writelane_b32 %1, %3, %8\n\t"
+        asm volatile(BA_WRITELANE_NOP "v_writelane_b32 %0, %2, %8\n\tv_writelane_b32 %1, %3, %8\n\t"
                      "v_writelane_b32 %0, %4, %9\n\tv_writelane_b32 %1, %5, %9\n\t"
                      "v_writelane_b32 %0, %6, %10\n\tv_writelane_b32 %1, %7, %10"
                      : "+v"(lo), "+v"(hi)
                      : "s"(l0), "s"(h0), "s"(l1), "s"(h1), "s"(l2), "s"(h2), "i"(G0), "i"(G0 + 1),
                        "i"(G0 + 2));
     else if constexpr (CNT == 2)
-        asm volatile("s_nop 4\n\tv_writelane_b32 %0, %2, %6\n\tv_writelane_b32 %1, %3, %6\n\t"
+        asm volatile(BA_WRITELANE_NOP "v_writelane_b32 %0, %2, %6\n\tv_writelane_b32 %1, %3, %6\n\t"
                      "v_writelane_b32 %0, %4, %7\n\tv_writelane_b32 %1, %5, %7"
                      : "+v"(lo), "+v"(hi)
                      : "s"(l0), "s"(h0), "s"(l1), "s"(h1), "i"(G0), "i"(G0 + 1));
     else
-        asm volatile("s_nop 4\n\tv_writelane_b32 %0, %2, %4\n\tv_writelane_b32 %1, %3, %4"
+        asm volatile(BA_WRITELANE_NOP "v_writelane_b32 %0, %2, %4\n\tv_writelane_b32 %1, %3, %4"
                      : "+v"(lo), "+v"(hi)
                      : "s"(l0), "s"(h0), "i"(G0));
     (void)l1; (void)h1; (void)l2; (void)h2; (void)l3; (void)h3;

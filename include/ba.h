@@ -23,7 +23,10 @@
  *     replay's ordering is the caller's.  So a stream that carried a call of
  *     a ctx must stay valid until that ctx's next call or ba_ctx_destroy.  Device
  *     buffers a captured graph holds stay valid until the ctx grows its
- *     scratch for a LARGER call: give a graph its own ctx.
+ *     scratch for a LARGER call: give a graph its own ctx.  Replays of graphs
+ *     captured from one ctx must not run concurrently with each other or with
+ *     an eager call of that ctx: they share the ctx's scratch, counter sink
+ *     and persistent-kernel task counter (one replay at a time per ctx).
  *
  * General indexing: the live generals sorted by id are
  * indexed 0..n-1; index 0 is the commander (lowest live id, ba.py:381 +

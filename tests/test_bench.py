@@ -60,3 +60,52 @@ def test_kernel_io_bytes_levels():
     assert bench.kernel_io_bytes("k_relay_top", 10, 3, 1 << 20, staged=True) == 8 * W * (9 + 72)
     assert bench.kernel_io_bytes("k_epilogue", 10, 3, 1 << 20, staged=True) == \
         8 * W * (9 + 72 + 13) + 9 * (1 << 20)
+
+
+def test_world_check_and_launch_command(monkeypatch):
+    """--gpus N: under a launcher the WORLD_SIZE must equal N (else exit code 2);
+    without one, N == 1 runs in-process and N > 1 starts torch.distributed.run on
+    N local ranks (127.0.0.1 rendezvous) as a child and returns its exit code."""
+    assert bench.check_or_launch_world(1, [], {}) is None
+    assert bench.check_or_launch_world(4, [], {"WORLD_SIZE": "4"}) is None
+    assert bench.check_or_launch_world(2, [], {"WORLD_SIZE": "3"}) == 2
+    assert bench.check_or_launch_world(1, [], {"WORLD_SIZE": "8"}) == 2
+    assert bench.check_or_launch_world(0, [], {}) == 2
+    cmd = bench.launch_cmd(8, ["--gpus", "8", "--steps", "5"], 29500)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert "--master-port=29500" in cmd and cmd[-4:] == ["--gpus", "8", "--steps", "5"]
+    assert cmd[-5].endswith("bench.py")
+    seen = {}
+
+    def fake_call(c, env):
+        seen["cmd"], seen["env"] = c, env
+        return 7
+    import subprocess
+    monkeypatch.setattr(subprocess, "call", fake_call)
+    assert bench.check_or_launch_world(2, ["--gpus", "2"], {"PATH": "/bin"}) == 7
+    assert "--nproc-per-node=2" in seen["cmd"] and seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_bench_exits_nonzero_on_world_mismatch():
+    """The script itself, before importing torch or touching a GPU."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=3" in r.stderr
+
+
+def test_cpu_baseline_checks_counters_against_gpu():
+    """The CPU leg runs the GPU's timed trial range first and compares all 12
+    counters; a mismatch is a hard failure (SystemExit)."""
+    import oracle_c
+    n, m, first, count = 10, 3, 64 * 1000, 64 * 50
+    _, _, want = oracle_c.run(n, m, count, seed=5, faulty_mode=1, f=3, order_mode=1,
+                              first_trial=first)
+    cpu = bench.run_cpu_baseline(n, m, 5, 3, 0.0, first, count, dict(want))
+    assert cpu["counters_match"] is True and cpu["counters_checked"]["trials"] == count
+    assert cpu["value"] > 0 and cpu["kind"] == "port"
+    bad = dict(want, agreement=want["agreement"] + 1)
+    with pytest.raises(SystemExit):
+        bench.run_cpu_baseline(n, m, 5, 3, 0.0, first, count, bad)

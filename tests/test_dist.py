@@ -325,9 +325,10 @@ def test_second_hop_votes_match_oracle_gpu(engine, n, m, B, nr):
 
 @pytest.mark.gpu
 def test_split_multi_world1_equals_unsplit_n16_m5(engine):
-    """Config 5 through ba_run_instance_split_multi (one-rank RCCL communicator: the
-    grouped broadcast runs, with one root) equals ba_run_trials on the same params,
-    and equals the C port on the full 1024-instance batch."""
+    """Config 5 through ba_run_instance_split_multi on a one-rank RCCL communicator
+    equals ba_run_trials on the same params, and equals the C port on the full
+    1024-instance batch.  At one rank the entry takes the unsplit pass (no vote
+    array, no broadcast); test_forced_split_world1_* below runs the exchange."""
     from ba_amd import dist as D
     from ba_amd import lib as L
     dev = torch.device("cuda", 0)
@@ -345,6 +346,71 @@ def test_split_multi_world1_equals_unsplit_n16_m5(engine):
         od, oo, oc = oracle_c.sliced_run(16, 5, B, seed=0xBA5EED, faulty_mode=1, f=5,
                                          order_mode=1)
         assert np.array_equal(ref.decisions, od) and np.array_equal(ref.outcome, oo)
+        assert {k: cnt[k] for k in oc} == oc
+    finally:
+        comm.close()
+
+
+@pytest.fixture
+def force_split(monkeypatch):
+    """BA_FORCE_SPLIT=1 (test-only, read by libba_hip on every call): the split
+    entry takes the vote-array path at one rank -- the vote buffer, the
+    pre-exchange error agreement, the grouped ncclBroadcast all-gather and the
+    error all-reduce of finish_job all run on the real one-rank communicator."""
+    monkeypatch.setenv("BA_FORCE_SPLIT", "1")
+    yield
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("level", [1, 2])
+def test_forced_split_world1_matches_oracle(engine, force_split, level):
+    """Config 5 (n=16, m=5), batch 70, through ba_run_instance_split_level_multi with
+    the split forced at world 1: decisions, outcome bytes and counters equal the
+    oracle (every rank's rows are its own, so the broadcast's layout -- rows
+    [ub*row, ue*row) of rank 0 -- must be the one the root pass reads)."""
+    from ba_amd import dist as D
+    from ba_amd import lib as L
+    dev = torch.device("cuda", 0)
+    kw = dict(seed=0xBA5EED, faulty_mode=L.FAULTY_RANDOM, f=5, order_mode=L.ORDER_RANDOM,
+              first_trial=64 * 7)
+    p = L.make_params(16, 5, **kw)
+    B = 70
+    comm = L.Comm(engine, 1, 0, L.comm_unique_id())
+    try:
+        for _ in range(2):  # the second call reuses the grown vote buffer
+            dec, out, cnt = D.run_instance_split(comm, p, B, dev, level=level)
+            od, oo, oc = oracle_c.run(16, 5, B, **kw)
+            assert np.array_equal(dec.cpu().numpy().view(np.uint64), od)
+            assert np.array_equal(out.cpu().numpy(), oo)
+            assert {k: cnt[k] for k in oc} == oc
+    finally:
+        comm.close()
+
+
+@pytest.mark.gpu
+def test_forced_split_world1_failure_before_exchange(engine, force_split, monkeypatch):
+    """A rank that cannot allocate its vote buffer (BA_TEST_VOTE_ENOMEM=1 injects
+    it) returns ENOMEM after the pre-exchange agreement instead of skipping the
+    broadcast its peers wait in; an invalid split level fails the same way; the
+    communicator stays usable and the next call is exact."""
+    from ba_amd import dist as D
+    from ba_amd import lib as L
+    dev = torch.device("cuda", 0)
+    kw = dict(seed=3, faulty_mode=L.FAULTY_RANDOM, f=3, order_mode=L.ORDER_RANDOM)
+    p = L.make_params(10, 3, **kw)
+    comm = L.Comm(engine, 1, 0, L.comm_unique_id())
+    try:
+        monkeypatch.setenv("BA_TEST_VOTE_ENOMEM", "1")
+        with pytest.raises(L.BAError) as ei:
+            D.run_instance_split(comm, p, 100, dev, level=2)
+        assert ei.value.code == L.ENOMEM
+        monkeypatch.delenv("BA_TEST_VOTE_ENOMEM")
+        with pytest.raises(L.BAError) as ei:
+            D.run_instance_split(comm, p, 100, dev, level=3)
+        assert ei.value.code == L.EINVAL
+        dec, out, cnt = D.run_instance_split(comm, p, 100, dev, level=2)
+        od, oo, oc = oracle_c.run(10, 3, 100, **kw)
+        assert np.array_equal(dec.cpu().numpy().view(np.uint64), od)
         assert {k: cnt[k] for k in oc} == oc
     finally:
         comm.close()

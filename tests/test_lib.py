@@ -91,3 +91,40 @@ def test_trial_share_partitions():
             assert pos == total
     with pytest.raises(L.BAError):
         L.trial_share(10, 2, 2)
+
+
+def test_writelane_wait_states_in_shipped_library():
+    """Every v_writelane_b32 in libba_hip.so whose data SGPR was written by a VALU
+    instruction (the WAVE kernels' ballots -> writelane4, and the compiler's own
+    SGPR spills) has the wait states the hardware needs between the two
+    (tests/codeobj.py), and the staged-input k_om3w<10> -- the bench kernel --
+    contains such pairs at all."""
+    import codeobj
+    found_bench_kernel = False
+    for co in codeobj.code_objects():
+        for name, ins in codeobj.functions(codeobj.disassemble(co)).items():
+            bad, checked = codeobj.writelane_hazards(ins)
+            assert not bad, (name, bad[:3])
+            if name.startswith("_ZN2ba6k_om3wILi10ELi0ELb1EE"):
+                found_bench_kernel = checked > 0
+    assert found_bench_kernel
+
+
+def test_writelane_check_catches_missing_nop(tmp_path):
+    """The same check fails on a build of the bench kernel whose writelane4 groups
+    lack their s_nop (tests/native/writelane_probe.hip with BA_WRITELANE_NOP
+    empty), and passes on the same probe built as shipped."""
+    import subprocess
+    import codeobj
+    src = os.path.join(ROOT, "tests", "native", "writelane_probe.hip")
+    res = {}
+    for tag, extra in (("nop", []), ("nonop", ['-DBA_WRITELANE_NOP=""'])):
+        out = str(tmp_path / f"{tag}.co")
+        subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950",
+                        "--cuda-device-only", "--no-gpu-bundle-output", "-o", out, src] + extra,
+                       check=True, capture_output=True)
+        fns = codeobj.functions(codeobj.disassemble(open(out, "rb").read()))
+        (ins,) = [v for k, v in fns.items() if k.startswith("_ZN2ba6k_om3wILi10ELi0ELb1EE")]
+        res[tag] = codeobj.writelane_hazards(ins)
+    assert res["nop"][0] == [] and res["nop"][1] > 0
+    assert len(res["nonop"][0]) > 0 and min(b[3] for b in res["nonop"][0]) < 2

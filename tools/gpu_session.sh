@@ -2,7 +2,7 @@
 # GPU-box session: every GPU step has its own time limit; a fault, abort or
 # timeout ends the session (no retries).  Logs land in gpurun_out/.
 # usage: tools/gpu_session.sh [stage ...]
-#   tests smoke bench bench_levels bench_fused prof prof1 pmc philox configs
+#   tests smoke bench bench2 bench_levels bench_fused prof prof1 pmc philox configs
 #   (prof: the default bench command, two steps in flight, so each k_om3w launch
 #   spans ~2x its own time; prof1: --streams 1, the launch time the roofline uses)
 set -u
@@ -32,6 +32,7 @@ for s in $STAGES; do
     tests) run pytest_gpu 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) run bench 600 python -u bench.py --steps 20 --warmup 3 || exit $? ;;
+    bench2) run bench2 600 env BA_BENCH_DEVICE=0 python -u bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu || exit $? ;;
     bench_levels) run bench_levels 600 python -u bench.py --steps 20 --warmup 3 --engine levels --no-cpu || exit $? ;;
     bench_fused) run bench_fused 600 python -u bench.py --steps 20 --warmup 3 --engine fused --no-cpu || exit $? ;;
     philox) run philox 120 ./tools/philox_bench || exit $? ;;
