@@ -6,7 +6,7 @@ exits if killed, and -- unless it is primary -- connects to its primary_port as
 a heartbeat (ba.py:306-310); a failed connect starts an election (`elect`,
 ba.py:126-157: win if no reachable general has a lower id, then broadcast
 `new_leader` and become primary for life).  The same loop computes a
-lieutenant's majority once an order has arrived (ba.py:316-317), and the REPL
+lieutenant's majority once an order has arrived (ba.py:318-319), and the REPL
 waits for each general's majority by polling every 0.1 s (`wait_majority`,
 ba.py:287-289).  So what ba.py prints depends on WHEN commands arrive relative
 to those ticks: a `g-state` typed before the first tick shows every general
@@ -20,7 +20,7 @@ a killed primary is replaced one tick later by the lowest live id.
     `g-add` for later ones), plus an optional deterministic per-general phase
     (`jitter`, seeded) standing in for thread start-up skew;
   * ticks are processed in time order (ties: lower id first), each running
-    ba.py:303-317 on the membership state of `generals.Cluster`, which already
+    ba.py:303-319 on the membership state of `generals.Cluster`, which already
     restates discover_leader / elect / kill / add exactly;
   * RPCs take zero virtual time (ba.py's localhost connects are ~ms against the
     100 ms ticks).
@@ -69,7 +69,7 @@ class TimedCluster(Cluster):
         self.events.append((round(self.now, 9), kind, g.id, detail))
 
     def _tick(self, g: General):
-        """One iteration of Process.run after its sleep (ba.py:303-317)."""
+        """One iteration of Process.run after its sleep (ba.py:303-319)."""
         if g.killed:  # ba.py:303-304: the thread exits
             self._dead.pop(g.port, None)
             self._log("exit", g)
@@ -79,7 +79,7 @@ class TimedCluster(Cluster):
                 self._log("heartbeat-fail", g, str(g.primary_port))
                 self._elect(g)
                 self._log("elect-win" if g.primary else "elect-lose", g)
-            if self.pending.get(g.port):  # ba.py:316-317: the majority is taken now
+            if self.pending.get(g.port):  # ba.py:318-319: the majority is taken now
                 self.pending[g.port] = False
                 self._log("majority", g)
         return True
@@ -130,8 +130,8 @@ class TimedCluster(Cluster):
     def round_timing(self) -> float:
         """Issue an order at the current time and advance the clock through the
         REPL's wait_majority loop (ba.py:287-289, in process order); returns the
-        round's virtual latency.  The primary decides at once (ba.py:282-283),
-        a lieutenant at its next tick (ba.py:316-317)."""
+        round's virtual latency.  The primary decides at once (ba.py:285),
+        a lieutenant at its next tick (ba.py:318-319)."""
         t0 = self.now
         for g in self.processes[1:]:
             self.pending[g.port] = True

@@ -218,6 +218,7 @@ struct ba_ctx {
     bool leaf_fusion = true;  // LEVELS uses k_leaf when available (BA_NO_LEAF_FUSION=1: off)
     DevBuf scratch, partials, io_faulty, io_order, io_table, io_poll, io_dec, io_out, io_cnt;
     DevBuf sink;  // counter sink replicas (zeroed once; kernels leave them zero)
+    DevBuf casc;  // k_cascade's fan-in counters (zeroed when grown; kernels leave them zero)
     std::map<uint64_t, std::unique_ptr<GeoEntry>> geos;
     Prof prof;
     std::map<std::string, ProfTotal> prof_totals;
@@ -392,7 +393,7 @@ extern "C" void ba_ctx_destroy(ba_ctx* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     prof_collect(ctx);
     for (hipEvent_t e : ctx->prof.pool) (void)hipEventDestroy(e);
-    for (DevBuf* b : {&ctx->sink, &ctx->scratch, &ctx->partials, &ctx->io_faulty, &ctx->io_order, &ctx->io_table,
+    for (DevBuf* b : {&ctx->sink, &ctx->casc, &ctx->scratch, &ctx->partials, &ctx->io_faulty, &ctx->io_order, &ctx->io_table,
                       &ctx->io_poll, &ctx->io_dec, &ctx->io_out, &ctx->io_cnt})
         b->release();
     for (auto& kv : ctx->geos) {
@@ -574,6 +575,46 @@ static int run_levels(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge, const LevelsJ
     return BA_OK;
 }
 
+// LEVELS in one launch per chunk (k_cascade, ba_cascade.hip): chunked like
+// run_levels, with its own scratch plan (R_1 .. R_{me-2}, word-major) and the
+// ctx's fan-in counters.  BA_NO_CASCADE=1 keeps the multi-launch pipeline (A/B).
+static bool use_cascade(ba_ctx* ctx, const Geometry& g) {
+    const char* e = getenv("BA_NO_CASCADE");  // read per call: tests switch it in-process
+    const bool off = e && atoi(e) != 0;
+    return !off && ctx->leaf_fusion && leaf_supported(g) && g.me >= 3 && cascade_supported(g);
+}
+
+static int run_cascade(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge) {
+    const Geometry& g = ge->g;
+    const uint64_t per_word = cascade_scratch_words_per_word(g) * sizeof(uint64_t);
+    const uint64_t words = (a.batch + 63) / 64;
+    uint64_t max_level = 0;
+    for (uint32_t k = 0; k + 2 <= g.me; ++k) max_level = g.S[k] > max_level ? g.S[k] : max_level;
+    uint64_t chunk = ctx->scratch_budget / (per_word ? per_word : 1);
+    const uint64_t idx_cap = (1ull << 31) / (max_level + 1);  // 32-bit slot indices in the kernel
+    if (chunk > idx_cap) chunk = idx_cap;
+    if (chunk > words) chunk = words;
+    if (chunk == 0)
+        return fail(BA_ETOOBIG, "one 64-trial word needs %llu bytes of scratch (budget %zu)",
+                    (unsigned long long)per_word, ctx->scratch_budget);
+    int rc;
+    if ((rc = ctx->scratch.grow(chunk * per_word)) != BA_OK) return rc;
+    const size_t cbytes = chunk * cascade_counters_per_word(g) * 128;
+    if (cbytes > ctx->casc.bytes) {
+        if ((rc = ctx->casc.grow(cbytes)) != BA_OK) return rc;
+        HIP_TRY(hipMemset(ctx->casc.p, 0, ctx->casc.bytes));  // kernels leave them zero
+        HIP_TRY(hipDeviceSynchronize());  // the launch stream is non-blocking
+    }
+    for (uint64_t w0 = 0; w0 < words; w0 += chunk) {
+        const uint64_t wn = (words - w0) < chunk ? (words - w0) : chunk;
+        const uint64_t trial0 = w0 * 64;
+        const uint64_t nt = (a.batch - trial0) < wn * 64 ? (a.batch - trial0) : wn * 64;
+        HIP_TRY(launch_cascade(a, g, (const uint8_t*)ge->sender.p, (uint64_t*)ctx->scratch.p,
+                               (uint32_t*)ctx->casc.p, trial0, nt));
+    }
+    return BA_OK;
+}
+
 static int run_trials_device_impl(ba_ctx* ctx, const ba_params* p, uint64_t batch,
                                   const uint32_t* d_faulty, const uint8_t* d_order,
                                   const uint32_t* d_table, const uint32_t* d_poll,
@@ -609,6 +650,7 @@ static int run_trials_device_impl(ba_ctx* ctx, const ba_params* p, uint64_t batc
                              (const uint8_t*)ge->sender.p, partials));
         return BA_OK;
     }
+    if (use_cascade(ctx, g)) return run_cascade(ctx, a, ge);
     return run_levels(ctx, a, ge, LevelsJob{}, 0, g.L, false, partials);
 }
 

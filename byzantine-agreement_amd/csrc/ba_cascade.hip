@@ -1,0 +1,593 @@
+// ba_cascade.hip -- the LEVELS tree in ONE launch (gfx950): k_cascade<N, ME>.
+//
+// The multi-launch LEVELS pipeline for an OM(me) tree (n=16, m=5: k_input,
+// k_relay_top, k_leaf_up, k_majority, k_tail) spends a third of a 1024-instance
+// call in short latency-bound launches and their gaps.  Here
+// every majority level above the leaf blocks is taken by whichever wave
+// finishes the LAST input of it -- a fan-in cascade inside the launch, no grid
+// barrier and no waiting anywhere:
+//
+//   unit (word w, level-Q slot rho; Q = me-3), G = S+1 lanes, one leaf block
+//   each (the leaf-up kernel's unit, ba_fused.hip k_leaf_up):
+//     inputs   the block bit-slices the trials of its words into LDS once
+//     chain    L_0 .. L_{me-2} of the lane's slot sr = rho.x, relayed from the
+//              commander down (one Philox pair per level, ba.py:42-57, 257-285)
+//     leaf     relay levels me-1, me and the leaf majorities (leaf_block<S>)
+//     up       R_{me-2}[rho.x] = maj(L_{me-2}[rho.x], R_{me-1}[rho.a.x] : a != x)
+//   then arrives at the counter of rho's parent sigma.  The arrival that
+//   completes sigma's children runs step q = Q for sigma:
+//     R_q[sigma.r] = maj(L_q[sigma.r], R_{q+1}[sigma.j.r] : j != r)
+//   (ba.py:159-195 generalised, inner tie -> non-attack), arrives at sigma's
+//   parent, and so on up to q = 0: the root majorities (tie -> undefined) and
+//   the quorum epilogue of the word (ba.py:197-255, wave_epilogue).
+//
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, table row 1):
+// results are stored write-through (sc1: relaxed agent-scope atomic stores),
+// the storing wave drains vmcnt, then ONE lane adds to the parent's counter
+// (agent scope); the wave whose add returns the last count reads the children
+// with sc1 loads only, after its add returned.  Counters sit on 128-B lines of
+// their own; the last arriver resets its counter, so the buffer is zero between
+// calls (zeroed once when the ctx allocates it).
+//
+// Bit-identical to the LEVELS pipeline: same lie keying (level, global slot
+// pair, global word), same majorities and epilogue.
+#include "ba_wave.hpp"
+
+namespace ba {
+
+constexpr int kCascMaxLevels = 8;
+constexpr uint32_t kCascCounterStride = 32;  // uint32 per counter: one 128-B line each
+
+struct CascArgs {
+    uint64_t seed;
+    GenSpec gs;
+    uint64_t first_trial;  // global index of the chunk's trial 0
+    uint64_t ntrials;      // trials of this chunk
+    uint32_t W;            // words of this chunk
+    uint32_t units;        // W * |L_Q|
+    const uint32_t* faulty;  // chunk-relative (GIVEN), or nullptr
+    const uint8_t* order;
+    const uint8_t* sender;   // Geometry::sender
+    uint32_t snd_off[kCascMaxLevels];
+    const uint64_t* members;  // level me-2 leaf-block member ids, 5 bits each
+    uint64_t* R[kCascMaxLevels];  // R_k, k = 1..me-2: [W][|L_k|] (word-major)
+    uint32_t* cnt;                // counters [..] x kCascCounterStride
+    uint32_t cnt_off[kCascMaxLevels];  // level k (0..Q-1) counters of word w at cnt_off[k] + w*|L_k|;
+                                       // cnt_off[Q]: the word's root counter at cnt_off[Q] + w
+    uint64_t* decisions;  // chunk-relative
+    uint8_t* outcome;
+    uint64_t* counters;
+    Sink sk;
+};
+
+// |L_k| = P(L, k+1)
+constexpr uint32_t casc_sz(int L, int k) {
+    uint32_t p = 1;
+    for (int i = 0; i <= k; ++i) p *= (uint32_t)(L - i);
+    return p;
+}
+
+template <int N, int ME>
+struct Casc {
+    static constexpr int L = N - 1, S = N - ME, G = S + 1, GP = G + 1, GPW = 64 / G;
+    static constexpr int Q = ME - 3, NIN = N + 3;
+    static constexpr uint32_t sz(int k) { return casc_sz(L, k); }
+    static constexpr int tr_words = GPW * G * GP;  // per wave: [unit][receiver][sender] transpose
+    // words a block-iteration's 4 * GPW units can span (NSL per slicing wave),
+    // and the triple-buffered input planes
+    static constexpr uint32_t nw_max = (4u * GPW + casc_sz(L, Q) - 1) / casc_sz(L, Q) + 1;
+    static constexpr int NSL = (int)(nw_max + 3) / 4;
+    static constexpr uint32_t planes_words = (3u * nw_max * NIN + 1u) & ~1u;
+};
+
+__device__ __forceinline__ uint64_t sel64(uint64_t f, uint64_t a, uint64_t b) { return (f & a) | (~f & b); }
+
+// the lie word of level-k slot x of trial word gw: half x%2 of Philox pair x/2
+__device__ __forceinline__ uint64_t lie_word(uint64_t seed, uint32_t k, uint32_t x, uint64_t gw) {
+    uint64_t l0, l1;
+    lie_pair(seed, k, x >> 1, gw, l0, l1);
+    return (x & 1u) ? l1 : l0;
+}
+
+// L_K[x] (level-K slot x) of the word whose planes are `in`: the relay chain
+// from the commander (L_0 = commander's coin or order, ba.py:263-285), each
+// level relayed by the last general of the slot above (ba.py:42-57).
+template <int N, int K>
+__device__ __forceinline__ uint64_t chain_value(const CascArgs& a, const uint64_t* in, uint32_t x,
+                                                uint64_t gw) {
+    constexpr int L = N - 1;
+    uint32_t anc[K + 1];
+    anc[K] = x;
+    static_for<0, K>([&](auto i) {
+        constexpr int k = K - 1 - i();
+        anc[k] = anc[k + 1] / (uint32_t)(L - (k + 1));
+    });
+    uint64_t v = in[N];  // OB
+    static_for<0, K + 1>([&](auto k) {
+        uint32_t snd = 0;  // level 0: the commander relays
+        if constexpr (k() > 0) snd = a.sender[a.snd_off[k() - 1] + anc[k() - 1]];
+        v = sel64(in[snd], lie_word(a.seed, k(), anc[k()], gw), v);
+    });
+    return v;
+}
+
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ void store_sc1(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint64_t load_sc1(const uint64_t* p) {
+    return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One arrival at counter c (lane 0 adds; every lane gets the answer): true on
+// the arrival that completes `expect`, which also resets the counter.
+__device__ __forceinline__ bool arrive_last(uint32_t* c, uint32_t expect, uint32_t lane) {
+    uint32_t old = 0;
+    if (lane == 0)
+        old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
+    const bool last = old + 1 == expect;
+    if (last && lane == 0) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // compiler ordering only: no load of the children may move above the add
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return last;
+}
+
+// Lieutenant indices j[0..K] of the path of level-K slot x (lexicographic rank
+// over (K+1)-permutations of the L lieutenants): digit k is the rank of j[k]
+// among the lieutenants not in j[0..k-1], picked by one compare-increment per
+// earlier pick against the picks kept sorted (srt, ascending).
+template <int L, int K>
+__device__ __forceinline__ void unrank_path(uint32_t x, uint32_t (&j)[K + 1], uint32_t (&srt)[K + 1]) {
+    uint32_t c[K + 1];
+    static_for<0, K>([&](auto i) {
+        constexpr int k = K - i();
+        c[k] = x % (uint32_t)(L - k);
+        x /= (uint32_t)(L - k);
+    });
+    c[0] = x;
+    static_for<0, K + 1>([&](auto k) {
+        uint32_t pos = c[k()];
+        static_for<0, k()>([&](auto i) { pos += srt[i()] <= pos ? 1u : 0u; });
+        j[k()] = pos;
+        uint32_t v = pos;  // sorted insert
+        static_for<0, k()>([&](auto i) {
+            const uint32_t lo = srt[i()] < v ? srt[i()] : v, hi = srt[i()] < v ? v : srt[i()];
+            srt[i()] = lo;
+            v = hi;
+        });
+        srt[k()] = v;
+    });
+}
+
+// Relay values of NS consecutive level-KS slots base..base+NS-1 below the
+// level-(KS-1) slot `s` (or below the commander at KS = 0), one per lane of a
+// group of NL lanes (lane t < NS: slot base + t), drawn cooperatively: the
+// distinct Philox pairs -- the pairs of the NS slots and one pair per ancestor
+// level of s -- are spread over the group's lanes (call c on lane c % NL),
+// exchanged through the group's LDS `xch` (>= 2 * (NPR + KS) words), and every
+// lane relays the chain down from the commander (ba.py:257-285, 42-57).
+// path: the lieutenants of s (j[0..KS-1]); inactive lanes draw but never
+// write; every lane of the wave must call it.
+template <int N, int KS, int NS, int NL>
+__device__ __forceinline__ uint64_t relay_slots(const CascArgs& a, const uint64_t* in, uint64_t* xch,
+                                                uint32_t t, bool active, uint32_t s, uint32_t base,
+                                                const uint32_t* path, uint64_t gw) {
+    constexpr int L = N - 1;
+    constexpr int NPR = NS / 2 + 1;  // pairs the NS slots can touch
+    constexpr int CALLS = NPR + KS, ROUNDS = (CALLS + NL - 1) / NL;
+    uint32_t anc[KS > 0 ? KS : 1];
+    if constexpr (KS > 0) {
+        anc[KS - 1] = s;
+        static_for<0, KS - 1>([&](auto i) {
+            constexpr int k = KS - 2 - i();
+            anc[k] = anc[k + 1] / (uint32_t)(L - (k + 1));
+        });
+    }
+    const uint32_t p0 = base >> 1;
+    static_for<0, ROUNDS>([&](auto rd) {
+        const uint32_t c = t + (uint32_t)(rd() * NL);  // this lane's call
+        uint32_t lvl = KS, pair = p0 + c;
+        static_for<0, KS>([&](auto k) {
+            if (c == (uint32_t)(NPR + k())) {
+                lvl = k();
+                pair = anc[k()] >> 1;
+            }
+        });
+        uint64_t l0, l1;
+        lie_pair(a.seed, lvl, pair, gw, l0, l1);
+        if (active && c < (uint32_t)CALLS) {
+            xch[2 * c] = l0;
+            xch[2 * c + 1] = l1;
+        }
+    });
+    __builtin_amdgcn_wave_barrier();
+    uint64_t v = in[N];  // OB: the commander's order
+    static_for<0, KS>([&](auto k) {
+        uint32_t snd = 0;  // level 0: the commander relays
+        if constexpr (k() > 0) snd = path[k() - 1] + 1;
+        v = sel64(in[snd], xch[2 * (NPR + k()) + (anc[k()] & 1u)], v);
+    });
+    const uint32_t x = base + (t < (uint32_t)NS ? t : 0u);
+    uint32_t snd = 0;
+    if constexpr (KS > 0) snd = path[KS - 1] + 1;
+    const uint64_t r = sel64(in[snd], xch[2 * ((x >> 1) - p0) + (x & 1u)], v);
+    __builtin_amdgcn_wave_barrier();  // xch is reused by the caller
+    return r;
+}
+
+// Step q for sigma (level q-1 slot s; q = 0: the word's roots), run by one
+// whole wave, lane r = receiver index among the K = L - q lieutenants not in
+// sigma.  in: the word's input planes (LDS); scr: the wave's LDS scratch.
+template <int N, int ME, int q>
+__device__ __noinline__ void casc_step(const CascArgs& a, const uint64_t* in, uint64_t* scr,
+                                          uint32_t lane, uint32_t w, uint32_t s, uint64_t gw,
+                                          TrialCounts& tc) {
+    using C = Casc<N, ME>;
+    constexpr int L = C::L, K = L - q;
+    const bool act = lane < (uint32_t)K;
+    const uint32_t r = act ? lane : 0u;
+    // L_q[sigma.r], sigma's path unranked (no tables)
+    uint32_t path[q > 0 ? q : 1], srt[q > 0 ? q : 1];
+    if constexpr (q > 0) unrank_path<L, q - 1>(s, path, srt);
+    const uint64_t lq = relay_slots<N, q, K, 64>(a, in, scr, lane, true, s, s * (uint32_t)K, path, gw);
+    // R_{q+1}[sigma.j.r], j != r: child c = r - (r > j) of level-q slot s*K + j
+    const uint64_t* Rc = a.R[q + 1] + (uint64_t)w * C::sz(q + 1);
+    uint64_t cv[K - 1];
+    static_for<0, K - 1>([&](auto jj) {
+        const uint32_t j = (uint32_t)jj() + ((uint32_t)jj() >= r ? 1u : 0u);
+        const uint32_t idx = (s * (uint32_t)K + j) * (uint32_t)(K - 1) + r - (r > j ? 1u : 0u);
+        cv[jj()] = act ? load_sc1(Rc + idx) : 0ull;
+    });
+    Csa<planes_c(K)> cnt;
+    cnt.template add<0>(lq);
+    static_for<0, K - 1>([&](auto jj) { cnt.template add<jj() + 1>(cv[jj()]); });
+    if constexpr (q > 0) {
+        const uint64_t rq = cnt.template ge<K, K / 2 + 1>();  // inner tie -> non-attack
+        if (act) store_sc1(a.R[q] + (uint64_t)w * C::sz(q) + s * (uint32_t)K + r, rq);
+        drain_stores();
+        // arrive at sigma's parent (level q-2), or at the word's root counter
+        constexpr uint32_t up_fan = (uint32_t)(L - (q - 1));  // children of a level q-2 slot
+        const uint32_t ps = s / up_fan;
+        uint32_t* c;
+        if constexpr (q - 1 >= 1)
+            c = a.cnt + (uint64_t)(a.cnt_off[q - 2] + w * C::sz(q - 2) + ps) * kCascCounterStride;
+        else
+            c = a.cnt + (uint64_t)(a.cnt_off[C::Q] + w) * kCascCounterStride;
+        if (arrive_last(c, up_fan, lane)) casc_step<N, ME, q - 1>(a, in, scr, lane, w, ps, gw, tc);
+    } else {
+        constexpr int NIN = C::NIN;
+        const uint64_t att = cnt.template ge<K, K / 2 + 1>();
+        const uint64_t tie = (K % 2 == 0) ? (cnt.template ge<K, K / 2>() & ~att) : 0ull;
+        // the epilogue overwrites bytes of its input planes: a private copy
+        if (lane < (uint32_t)NIN) scr[lane] = in[lane];
+        if (act) {
+            scr[NIN + r] = att;
+            scr[NIN + L + r] = tie;
+        }
+        __builtin_amdgcn_wave_barrier();
+        wave_epilogue<N, 1, (uint32_t)ME, 0>(scr, scr + NIN, lane, w, a.ntrials, a.decisions,
+                                            a.outcome, tc);
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// Staged inputs of one word, loaded a block-iteration ahead (lane = trial):
+// the faulty mask and order of trial w*64 + lane, and whether it exists.
+struct WordRegs {
+    uint32_t f, o;
+    bool v;
+};
+
+__device__ __forceinline__ WordRegs load_word(const CascArgs& a, uint32_t w, uint32_t lane) {
+    const uint64_t i = (uint64_t)w * 64 + lane;
+    WordRegs r{0, 0, i < a.ntrials};
+    if (r.v) {
+        r.f = a.faulty[i];
+        r.o = a.order[i];
+    }
+    return r;
+}
+
+// One word's bit planes from the lanes' trials (stage_words' ballots, ba_wave.hpp)
+template <int N>
+__device__ __forceinline__ void slice_word(uint64_t* dst, uint32_t lane, const WordRegs& t) {
+    constexpr int NIN = N + 3;
+    constexpr uint32_t FMASK = N >= 32 ? 0xFFFFFFFFu : ((1u << N) - 1u);
+    const uint32_t xbits = (t.f & FMASK) | (t.o == 1u ? 1u << N : 0u) | (t.o == 2u ? 2u << N : 0u) |
+                           (t.v ? 4u << N : 0u);
+    uint32_t lo = 0, hi = 0;
+    static_for<0, (NIN + 3) / 4>([&](auto grp) {
+        constexpr int g0 = 4 * grp();
+        uint64_t b[4];
+        static_for<0, 4>([&](auto j) { b[j()] = g0 + j() < NIN ? __ballot((xbits >> (g0 + j())) & 1u) : 0ull; });
+        writelane4<g0, (NIN - g0 < 4 ? NIN - g0 : 4)>(lo, hi, b);
+    });
+    if (lane < (uint32_t)NIN) dst[lane] = (uint64_t)hi << 32 | lo;
+}
+
+// A persistent launch: block b takes block-iterations b, b + grid, ...; one
+// block-iteration is 4 * GPW consecutive units (their words: <= NWM).  Per
+// iteration k, software-pipelined so that no wave waits on a store or an
+// atomic it has just issued:
+//   S  words of k bit-sliced into LDS planes[k % 3] (staged inputs: from
+//      registers loaded during k-1)
+//   D  the steps whose last arrival was made in iteration k-1 (their atomics
+//      returned long ago)
+//   U  the units of k (relay chain, leaf blocks, R_{me-2}) -- the long part
+//   W  drain: the stores of k-1 (issued before U) completed during U
+//   P  loads for k+1 (staged inputs, leaf-block members)
+//   A  arrivals for the units of k-1 (returning atomics, read in D of k+1)
+//   St R_{me-2} of k stored write-through
+// and after the last iteration the pending arrivals and steps.
+// DIAG (lab only, tools/casc_lab.py, BA_CASC_DIAG=2; wrong results): 2 = no
+// fan-in (units only).  The product uses 0.
+template <int N, int ME, int DIAG = 0>
+__global__ __launch_bounds__(256) void k_cascade(CascArgs a) {
+    using C = Casc<N, ME>;
+    constexpr int L = C::L, S = C::S, G = C::G, GP = C::GP, GPW = C::GPW, NIN = C::NIN, Q = C::Q;
+    constexpr uint32_t R = C::sz(Q);  // units per word
+    constexpr uint32_t PB = 4u * GPW;
+    constexpr uint32_t NWM = C::nw_max;
+    constexpr int NPD = (S + 1) / 2;
+    constexpr uint32_t fan = (uint32_t)(L - Q);  // children of a level Q-1 slot (or of the root)
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t* planes = lds;  // [3][NWM][NIN]
+    uint64_t* tr = lds + C::planes_words + wv * (uint32_t)C::tr_words;
+    const uint64_t gw0 = a.first_trial >> 6;
+    const bool staged = a.gs.faulty_mode == 0 && a.gs.order_mode == 0;
+    const uint32_t iters = (a.units + PB - 1) / PB;
+    const uint32_t g = lane / G, x = lane - g * G;
+    TrialCounts tc;
+    // the lane's unit of block-iteration `it`
+    auto unit_of = [&](uint32_t it, uint32_t& w, uint32_t& rho) -> bool {
+        const uint32_t u = it * PB + wv * GPW + g;
+        const bool ok = g < (uint32_t)GPW && u < a.units;
+        const uint32_t uu = ok ? u : 0u;
+        w = uu / R;
+        rho = uu - w * R;
+        return ok;
+    };
+    auto first_word = [&](uint32_t it) { return (it * PB) / R; };
+    // pipeline registers
+    constexpr int NSL = C::NSL;
+    WordRegs pf[NSL];
+    static_for<0, NSL>([&](auto i) { pf[i()] = WordRegs{0, 0, false}; });
+    uint64_t pf_mem = 0;
+    auto prefetch = [&](uint32_t it) {
+        const uint32_t wf = first_word(it), wl = (min(it * PB + PB, a.units) - 1u) / R;
+        static_for<0, NSL>([&](auto i) {
+            const uint32_t kw = wv + 4u * i();
+            if (staged && kw <= wl - wf) pf[i()] = load_word(a, wf + kw, lane);
+        });
+        uint32_t w, rho;
+        if (unit_of(it, w, rho)) pf_mem = a.members[rho * (uint32_t)G + x];
+    };
+    uint32_t it1 = 0xFFFFFFFFu, it2 = 0xFFFFFFFFu;  // iterations of the pending arrivals / steps
+    uint32_t old2 = 0;                              // returned counts of it2's arrivals (x == 0 lanes)
+    // D: the steps of the units of iteration `it` whose arrival returned the last count
+    auto steps = [&](uint32_t it, uint32_t old, uint32_t buf) {
+        uint32_t w, rho;
+        const bool ok = unit_of(it, w, rho);
+        uint64_t m = __ballot(ok && x == 0 && old + 1 == fan);
+        while (m) {  // wave-uniform: every lane runs each completed parent's step
+            const uint32_t b = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t wb = (uint32_t)__builtin_amdgcn_readlane((int)w, (int)b);
+            const uint32_t rb = (uint32_t)__builtin_amdgcn_readlane((int)rho, (int)b);
+            const uint64_t* inb = planes + (buf * NWM + (wb - first_word(it))) * NIN;
+            casc_step<N, ME, Q>(a, inb, tr, lane, wb, Q >= 1 ? rb / fan : 0u, gw0 + wb, tc);
+        }
+    };
+    // A: one lane per unit adds to the counter of rho's parent (level Q-1), or
+    // at Q = 0 of the word; returns the count before the add
+    auto arrive = [&](uint32_t it) -> uint32_t {
+        uint32_t w, rho, old = 0;
+        if (unit_of(it, w, rho) && x == 0) {
+            uint32_t* c;
+            if constexpr (Q >= 1)
+                c = a.cnt + (uint64_t)(a.cnt_off[Q - 1] + w * C::sz(Q - 1) + rho / fan) * kCascCounterStride;
+            else
+                c = a.cnt + (uint64_t)(a.cnt_off[0] + w) * kCascCounterStride;
+            old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (old + 1 == fan) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return old;
+    };
+    uint32_t k = 0;
+    if (blockIdx.x < iters) prefetch(blockIdx.x);
+    for (uint32_t it = blockIdx.x; it < iters; it += gridDim.x, ++k) {
+        const uint32_t buf = k % 3;
+        const uint32_t wfirst = first_word(it);
+        const uint32_t nw = (min(it * PB + PB, a.units) - 1u) / R - wfirst + 1u;
+        uint64_t* pl = planes + buf * NWM * NIN;
+        // S
+        static_for<0, NSL>([&](auto i) {
+            const uint32_t kw = wv + 4u * i();
+            if (kw < nw) {
+                if (staged) slice_word<N>(pl + kw * NIN, lane, pf[i()]);
+                else wave_inputs<N, 1, 0>(pl + kw * NIN, lane, wfirst + kw, a.seed, a.gs,
+                                          a.first_trial, a.ntrials, a.faulty, a.order);
+            }
+        });
+        const uint64_t mem = pf_mem;
+        __syncthreads();
+        // D
+        if constexpr ((DIAG & 2) == 0) {
+            if (it2 != 0xFFFFFFFFu) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                steps(it2, old2, (k + 1) % 3);  // it2 ran two iterations ago: buffer (k-2) % 3
+            }
+        }
+        // U
+        uint32_t w, rho;
+        const bool act = unit_of(it, w, rho);
+        const uint64_t* in = pl + (w - wfirst) * NIN;
+        const uint64_t gw = gw0 + w;
+        const uint32_t sr = rho * (uint32_t)G + x;  // the lane's level me-2 slot
+        const uint32_t gg = act ? g : 0u;
+        // (the leaf work sits in a divergent branch: as straight-line code for
+        // every lane the compiler's schedule needed 256 VGPRs and spilled)
+        if (act) {
+            uint32_t path[Q + 2], srt[Q + 2];
+            unrank_path<L, Q + 1>(sr, path, srt);
+            // L_{me-2}[rho.x]: the unit's G slots drawn together
+            const uint64_t par = relay_slots<N, Q + 1, G, G>(a, in, tr + gg * (G * GP), x, true, rho,
+                                                              rho * (uint32_t)G, path, gw);
+            const uint64_t fs = in[path[Q + 1] + 1];  // level me-1 relayer: the slot's last lieutenant
+            const uint32_t x0 = sr * (uint32_t)S;
+            uint64_t lw[2 * NPD];
+            lie_pairs<NPD>(a.seed, ME - 1, x0 >> 1, gw, lw);
+            const uint64_t oddmask = 0ull - (uint64_t)(x0 & 1u);
+            uint64_t diag[S], Fm[S], Rm[S];
+            static_for<0, S>([&](auto b) {
+                uint64_t lie;
+                if constexpr (S % 2 == 1) lie = lw[b()] ^ ((lw[b()] ^ lw[b() + 1]) & oddmask);
+                else lie = lw[b()];
+                diag[b()] = sel64(fs, lie, par);
+                Fm[b()] = in[(mem >> (5 * b())) & 31u];
+            });
+            leaf_block<S>(ME, a.seed, gw, sr, diag, Fm, Rm);
+            uint64_t* t = tr + (gg * G) * GP + x;
+            t[x * GP] = par;
+            static_for<0, S>([&](auto d) { t[(d() + (d() >= x ? 1u : 0u)) * GP] = Rm[d()]; });
+        }
+        __builtin_amdgcn_wave_barrier();
+        uint64_t rmaj = 0;
+        if (act) {
+            const uint64_t* col = tr + (gg * G + x) * GP;
+            Csa<planes_c(G)> cnt;
+            static_for<0, G>([&](auto b) { cnt.template add<b()>(col[b()]); });
+            rmaj = cnt.template ge<G, G / 2 + 1>();
+        }
+        __builtin_amdgcn_wave_barrier();
+        // W
+        drain_stores();
+        // P
+        if (it + gridDim.x < iters) prefetch(it + gridDim.x);
+        // A (iteration it1's units; their stores drained above)
+        if constexpr ((DIAG & 2) == 0) {
+            it2 = it1;
+            old2 = it1 != 0xFFFFFFFFu ? arrive(it1) : 0u;
+        }
+        // St
+        if (act) store_sc1(a.R[ME - 2] + (uint64_t)w * C::sz(ME - 2) + sr, rmaj);
+        it1 = it;
+    }
+    if constexpr ((DIAG & 2) == 0) {
+        // pending: the steps of it2 (atomics issued in the last iteration), the
+        // arrivals and steps of it1 (the last iteration)
+        const uint32_t kl = k == 0 ? 0u : k - 1;  // the last iteration's index
+        if (it2 != 0xFFFFFFFFu) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            steps(it2, old2, (kl + 2) % 3);  // it2 = iteration kl - 1
+        }
+        if (it1 != 0xFFFFFFFFu) {
+            drain_stores();
+            const uint32_t o = arrive(it1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            steps(it1, o, kl % 3);
+        }
+    }
+    wave_flush(tc, lane, wv, 4, a.counters, a.sk, false);
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+#define BA_CASC_SHAPES(X) X(16, 5) X(16, 4) X(16, 3) X(10, 3) X(9, 4) X(8, 5)
+
+bool cascade_supported(const Geometry& g) {
+#define BA_CASC_OK(nn, mm) if (g.n == nn && g.me == mm) return true;
+    BA_CASC_SHAPES(BA_CASC_OK)
+#undef BA_CASC_OK
+    return false;
+}
+
+// counters per word (units of kCascCounterStride uint32): every level-k slot,
+// k < me-3, plus the word's root counter
+uint64_t cascade_counters_per_word(const Geometry& g) {
+    uint64_t c = 1;
+    for (uint32_t k = 0; k + 3 < g.me; ++k) c += g.S[k];
+    return c;
+}
+
+uint64_t cascade_scratch_words_per_word(const Geometry& g) {
+    uint64_t s = 0;
+    for (uint32_t k = 1; k + 2 <= g.me; ++k) s += g.S[k];
+    return s;
+}
+
+template <int N, int ME, int DIAG = 0>
+static hipError_t launch_cascade_t(CascArgs& ca, uint32_t cu_count, hipStream_t st) {
+    using C = Casc<N, ME>;
+    constexpr uint32_t per_block = 4u * C::GPW;
+    const uint32_t iters = (ca.units + per_block - 1) / per_block;
+    const size_t lds = (size_t)(C::planes_words + 4u * C::tr_words) * sizeof(uint64_t);
+    // persistent: as many blocks as stay resident (block-iterations beyond
+    // that are taken in turn), never more than there are iterations
+    static int occ = 0;
+    if (occ == 0) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_cascade<N, ME, DIAG>, 256, lds) !=
+                hipSuccess ||
+            occ < 1)
+            occ = 1;
+    }
+    const uint32_t resident = (uint32_t)occ * cu_count;
+    const uint32_t blocks = iters < resident ? iters : resident;
+    hipLaunchKernelGGL((k_cascade<N, ME, DIAG>), dim3(blocks ? blocks : 1), dim3(256), lds, st, ca);
+    return hipGetLastError();
+}
+
+hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_sender,
+                          uint64_t* scratch, uint32_t* d_cnt, uint64_t trial0, uint64_t ntrials) {
+    CascArgs ca{};
+    const uint64_t W = (ntrials + 63) / 64;
+    ca.seed = a.seed;
+    ca.gs = a.gen;
+    ca.first_trial = a.first_trial + trial0;
+    ca.ntrials = ntrials;
+    ca.W = (uint32_t)W;
+    ca.units = (uint32_t)(W * g.S[g.me - 3]);
+    ca.faulty = a.faulty ? a.faulty + trial0 : nullptr;
+    ca.order = a.order ? a.order + trial0 : nullptr;
+    ca.sender = d_sender;
+    for (uint32_t k = 0; k < g.me && k < (uint32_t)kCascMaxLevels; ++k)
+        ca.snd_off[k] = (uint32_t)g.sender_off[k];
+    ca.members = a.members;
+    uint64_t off = 0;
+    for (uint32_t k = 1; k + 2 <= g.me; ++k) {
+        ca.R[k] = scratch + off;
+        off += W * g.S[k];
+    }
+    ca.cnt = d_cnt;
+    uint32_t coff = 0;
+    for (uint32_t k = 0; k + 3 < g.me; ++k) {
+        ca.cnt_off[k] = coff;
+        coff += (uint32_t)(W * g.S[k]);
+    }
+    ca.cnt_off[g.me - 3] = coff;  // root counters
+    ca.decisions = a.decisions ? a.decisions + trial0 : nullptr;
+    ca.outcome = a.outcome ? a.outcome + trial0 : nullptr;
+    ca.counters = a.counters;
+    ca.sk = a.sink;
+    ProfScope ps(a.prof, "k_cascade", a.stream);
+    if (const char* d = getenv("BA_CASC_DIAG")) {  // lab ablations, n=16 m=5 only
+        if (g.n == 16 && g.me == 5) switch (atoi(d)) {
+            case 2: return launch_cascade_t<16, 5, 2>(ca, a.cu_count, a.stream);
+            default: break;
+        }
+    }
+#define BA_CASC_LAUNCH(nn, mm) \
+    if (g.n == nn && g.me == mm) return launch_cascade_t<nn, mm>(ca, a.cu_count, a.stream);
+    BA_CASC_SHAPES(BA_CASC_LAUNCH)
+#undef BA_CASC_LAUNCH
+    return hipErrorInvalidValue;
+}
+
+}  // namespace ba

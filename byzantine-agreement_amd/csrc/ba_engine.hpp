@@ -151,6 +151,14 @@ hipError_t launch_epilogue_w(const RunArgs& a, const Geometry& g, uint64_t W,
                              const uint64_t* scratch, const LevelsLayout& lay, const uint64_t* C1,
                              uint64_t* decisions, uint8_t* outcome);
 
+// LEVELS in one launch (ba_cascade.hip): leaf-up units plus an in-launch
+// fan-in cascade of the majority levels above them, roots and quorum
+bool cascade_supported(const Geometry& g);
+uint64_t cascade_counters_per_word(const Geometry& g);       // 128-B counters per trial word
+uint64_t cascade_scratch_words_per_word(const Geometry& g);  // R_1..R_{me-2} words per trial word
+hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_sender,
+                          uint64_t* scratch, uint32_t* d_cnt, uint64_t trial0, uint64_t ntrials);
+
 hipError_t launch_table(const RunArgs& a, uint64_t* partials);
 hipError_t launch_gen_inputs(const RunArgs& a, uint32_t* faulty_out, uint8_t* order_out);
 hipError_t launch_levels_chunk(const RunArgs& a, const Geometry& g, const uint8_t* d_sender,

@@ -1,4 +1,5 @@
-"""Config 5 (n=16, m=5, one GPU) A/B of the LEVELS launch-fusion switches.
+"""Config 5 (n=16, m=5, one GPU) A/B of the LEVELS launch-fusion switches
+(default: the one-launch k_cascade; no_cascade: the multi-launch pipeline).
 
     python tools/config5_ab.py [--batches 1,1024] [--reps 200]
 
@@ -25,12 +26,13 @@ from ba_amd import lib as L  # noqa: E402
 
 SETTINGS = {
     "default": {},
+    "no_cascade": {"BA_NO_CASCADE": "1"},
     "no_input": {"BA_NO_INPUT_FUSION": "1"},
     "no_tail": {"BA_NO_TAIL": "1"},
     "no_input_no_tail": {"BA_NO_INPUT_FUSION": "1", "BA_NO_TAIL": "1"},
     "no_leaf_up": {"BA_NO_LEAF_UP": "1"},
 }
-SWITCHES = ("BA_NO_LEAF_UP", "BA_NO_INPUT_FUSION", "BA_NO_TAIL")
+SWITCHES = ("BA_NO_CASCADE", "BA_NO_LEAF_UP", "BA_NO_INPUT_FUSION", "BA_NO_TAIL")
 
 
 def main():
