@@ -37,6 +37,12 @@ namespace ba {
 
 constexpr int kCascMaxLevels = 8;
 constexpr uint32_t kCascCounterStride = 32;  // uint32 per counter: one 128-B line each
+// waves per block (one-wave blocks, so that a wave taking fan-in steps holds
+// only its own slot, measured no faster: 70.6 vs 69.9 us, n=16 m=5 x 1024)
+#ifndef BA_CASC_WAVES
+#define BA_CASC_WAVES 4
+#endif
+constexpr uint32_t kCascWaves = BA_CASC_WAVES;
 
 struct CascArgs {
     uint64_t seed;
@@ -73,11 +79,9 @@ struct Casc {
     static constexpr int Q = ME - 3, NIN = N + 3;
     static constexpr uint32_t sz(int k) { return casc_sz(L, k); }
     static constexpr int tr_words = GPW * G * GP;  // per wave: [unit][receiver][sender] transpose
-    // words a block-iteration's 4 * GPW units can span (NSL per slicing wave),
-    // and the triple-buffered input planes
-    static constexpr uint32_t nw_max = (4u * GPW + casc_sz(L, Q) - 1) / casc_sz(L, Q) + 1;
-    static constexpr int NSL = (int)(nw_max + 3) / 4;
-    static constexpr uint32_t planes_words = (3u * nw_max * NIN + 1u) & ~1u;
+    // words a block's 4 * GPW units can span, and their input planes
+    static constexpr uint32_t nw_max = (kCascWaves * GPW + casc_sz(L, Q) - 1) / casc_sz(L, Q) + 1;
+    static constexpr uint32_t planes_words = (nw_max * NIN + 1u) & ~1u;
 };
 
 __device__ __forceinline__ uint64_t sel64(uint64_t f, uint64_t a, uint64_t b) { return (f & a) | (~f & b); }
@@ -168,54 +172,76 @@ __device__ __forceinline__ void unrank_path(uint32_t x, uint32_t (&j)[K + 1], ui
 // level-(KS-1) slot `s` (or below the commander at KS = 0), one per lane of a
 // group of NL lanes (lane t < NS: slot base + t), drawn cooperatively: the
 // distinct Philox pairs -- the pairs of the NS slots and one pair per ancestor
-// level of s -- are spread over the group's lanes (call c on lane c % NL),
-// exchanged through the group's LDS `xch` (>= 2 * (NPR + KS) words), and every
-// lane relays the chain down from the commander (ba.py:257-285, 42-57).
-// path: the lieutenants of s (j[0..KS-1]); inactive lanes draw but never
-// write; every lane of the wave must call it.
-template <int N, int KS, int NS, int NL>
-__device__ __forceinline__ uint64_t relay_slots(const CascArgs& a, const uint64_t* in, uint64_t* xch,
-                                                uint32_t t, bool active, uint32_t s, uint32_t base,
-                                                const uint32_t* path, uint64_t gw) {
-    constexpr int L = N - 1;
-    constexpr int NPR = NS / 2 + 1;  // pairs the NS slots can touch
-    constexpr int CALLS = NPR + KS, ROUNDS = (CALLS + NL - 1) / NL;
+// level of s -- are spread over the group's lanes (call c on lane c % NL) and
+// exchanged through the group's LDS `xch` (>= 2 * (NPR + KS) words)
+// (relay_draw: no input planes needed), then every lane relays the chain down
+// from the commander (relay_apply, ba.py:257-285, 42-57).  path: the
+// lieutenants of s (j[0..KS-1]); inactive lanes draw but never write; every
+// lane of the wave must call both.
+template <int N, int KS, int NS>
+struct RelayPlan {
+    static constexpr int L = N - 1, NPR = NS / 2 + 1, CALLS = NPR + KS;
     uint32_t anc[KS > 0 ? KS : 1];
-    if constexpr (KS > 0) {
-        anc[KS - 1] = s;
-        static_for<0, KS - 1>([&](auto i) {
-            constexpr int k = KS - 2 - i();
-            anc[k] = anc[k + 1] / (uint32_t)(L - (k + 1));
-        });
+    uint32_t p0;
+    __device__ __forceinline__ RelayPlan(uint32_t s, uint32_t base) : p0(base >> 1) {
+        if constexpr (KS > 0) {
+            anc[KS - 1] = s;
+            static_for<0, KS - 1>([&](auto i) {
+                constexpr int k = KS - 2 - i();
+                anc[k] = anc[k + 1] / (uint32_t)(L - (k + 1));
+            });
+        }
     }
-    const uint32_t p0 = base >> 1;
+};
+
+template <int N, int KS, int NS, int NL>
+__device__ __forceinline__ void relay_draw(const CascArgs& a, const RelayPlan<N, KS, NS>& rp,
+                                           uint64_t* xch, uint32_t t, bool active, uint64_t gw) {
+    using RP = RelayPlan<N, KS, NS>;
+    constexpr int ROUNDS = (RP::CALLS + NL - 1) / NL;
     static_for<0, ROUNDS>([&](auto rd) {
         const uint32_t c = t + (uint32_t)(rd() * NL);  // this lane's call
-        uint32_t lvl = KS, pair = p0 + c;
+        uint32_t lvl = KS, pair = rp.p0 + c;
         static_for<0, KS>([&](auto k) {
-            if (c == (uint32_t)(NPR + k())) {
+            if (c == (uint32_t)(RP::NPR + k())) {
                 lvl = k();
-                pair = anc[k()] >> 1;
+                pair = rp.anc[k()] >> 1;
             }
         });
         uint64_t l0, l1;
         lie_pair(a.seed, lvl, pair, gw, l0, l1);
-        if (active && c < (uint32_t)CALLS) {
+        if (active && c < (uint32_t)RP::CALLS) {
             xch[2 * c] = l0;
             xch[2 * c + 1] = l1;
         }
     });
-    __builtin_amdgcn_wave_barrier();
+}
+
+template <int N, int KS, int NS>
+__device__ __forceinline__ uint64_t relay_apply(const RelayPlan<N, KS, NS>& rp, const uint64_t* in,
+                                                const uint64_t* xch, uint32_t t, uint32_t base,
+                                                const uint32_t* path) {
+    using RP = RelayPlan<N, KS, NS>;
     uint64_t v = in[N];  // OB: the commander's order
     static_for<0, KS>([&](auto k) {
         uint32_t snd = 0;  // level 0: the commander relays
         if constexpr (k() > 0) snd = path[k() - 1] + 1;
-        v = sel64(in[snd], xch[2 * (NPR + k()) + (anc[k()] & 1u)], v);
+        v = sel64(in[snd], xch[2 * (RP::NPR + k()) + (rp.anc[k()] & 1u)], v);
     });
     const uint32_t x = base + (t < (uint32_t)NS ? t : 0u);
     uint32_t snd = 0;
     if constexpr (KS > 0) snd = path[KS - 1] + 1;
-    const uint64_t r = sel64(in[snd], xch[2 * ((x >> 1) - p0) + (x & 1u)], v);
+    return sel64(in[snd], xch[2 * ((x >> 1) - rp.p0) + (x & 1u)], v);
+}
+
+template <int N, int KS, int NS, int NL>
+__device__ __forceinline__ uint64_t relay_slots(const CascArgs& a, const uint64_t* in, uint64_t* xch,
+                                                uint32_t t, bool active, uint32_t s, uint32_t base,
+                                                const uint32_t* path, uint64_t gw) {
+    const RelayPlan<N, KS, NS> rp(s, base);
+    relay_draw<N, KS, NS, NL>(a, rp, xch, t, active, gw);
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t r = relay_apply<N, KS, NS>(rp, in, xch, t, base, path);
     __builtin_amdgcn_wave_barrier();  // xch is reused by the caller
     return r;
 }
@@ -224,7 +250,7 @@ __device__ __forceinline__ uint64_t relay_slots(const CascArgs& a, const uint64_
 // whole wave, lane r = receiver index among the K = L - q lieutenants not in
 // sigma.  in: the word's input planes (LDS); scr: the wave's LDS scratch.
 template <int N, int ME, int q>
-__device__ __noinline__ void casc_step(const CascArgs& a, const uint64_t* in, uint64_t* scr,
+__device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in, uint64_t* scr,
                                           uint32_t lane, uint32_t w, uint32_t s, uint64_t gw,
                                           TrialCounts& tc) {
     using C = Casc<N, ME>;
@@ -276,225 +302,116 @@ __device__ __noinline__ void casc_step(const CascArgs& a, const uint64_t* in, ui
     }
 }
 
-// Staged inputs of one word, loaded a block-iteration ahead (lane = trial):
-// the faulty mask and order of trial w*64 + lane, and whether it exists.
-struct WordRegs {
-    uint32_t f, o;
-    bool v;
-};
-
-__device__ __forceinline__ WordRegs load_word(const CascArgs& a, uint32_t w, uint32_t lane) {
-    const uint64_t i = (uint64_t)w * 64 + lane;
-    WordRegs r{0, 0, i < a.ntrials};
-    if (r.v) {
-        r.f = a.faulty[i];
-        r.o = a.order[i];
-    }
-    return r;
-}
-
-// One word's bit planes from the lanes' trials (stage_words' ballots, ba_wave.hpp)
-template <int N>
-__device__ __forceinline__ void slice_word(uint64_t* dst, uint32_t lane, const WordRegs& t) {
-    constexpr int NIN = N + 3;
-    constexpr uint32_t FMASK = N >= 32 ? 0xFFFFFFFFu : ((1u << N) - 1u);
-    const uint32_t xbits = (t.f & FMASK) | (t.o == 1u ? 1u << N : 0u) | (t.o == 2u ? 2u << N : 0u) |
-                           (t.v ? 4u << N : 0u);
-    uint32_t lo = 0, hi = 0;
-    static_for<0, (NIN + 3) / 4>([&](auto grp) {
-        constexpr int g0 = 4 * grp();
-        uint64_t b[4];
-        static_for<0, 4>([&](auto j) { b[j()] = g0 + j() < NIN ? __ballot((xbits >> (g0 + j())) & 1u) : 0ull; });
-        writelane4<g0, (NIN - g0 < 4 ? NIN - g0 : 4)>(lo, hi, b);
-    });
-    if (lane < (uint32_t)NIN) dst[lane] = (uint64_t)hi << 32 | lo;
-}
-
-// A persistent launch: block b takes block-iterations b, b + grid, ...; one
-// block-iteration is 4 * GPW consecutive units (their words: <= NWM).  Per
-// iteration k, software-pipelined so that no wave waits on a store or an
-// atomic it has just issued:
-//   S  words of k bit-sliced into LDS planes[k % 3] (staged inputs: from
-//      registers loaded during k-1)
-//   D  the steps whose last arrival was made in iteration k-1 (their atomics
-//      returned long ago)
-//   U  the units of k (relay chain, leaf blocks, R_{me-2}) -- the long part
-//   W  drain: the stores of k-1 (issued before U) completed during U
-//   P  loads for k+1 (staged inputs, leaf-block members)
-//   A  arrivals for the units of k-1 (returning atomics, read in D of k+1)
-//   St R_{me-2} of k stored write-through
-// and after the last iteration the pending arrivals and steps.
-// DIAG (lab only, tools/casc_lab.py, BA_CASC_DIAG=2; wrong results): 2 = no
-// fan-in (units only).  The product uses 0.
+// One block = 4 * GPW consecutive units (their words: <= nw_max, sliced into
+// LDS once).  Per wave:
+//   1. every Philox draw that needs no input: the level me-1 diagonal lies of
+//      the lane's leaf block and the unit's relay-chain lies (relay_draw) --
+//      the slicing waves' input loads land meanwhile
+//   2. inputs bit-sliced (one wave per word), block barrier
+//   3. relay chain, leaf block, R_{me-2}[rho.x] = maj over the unit's
+//      transpose, stored write-through
+//   4. drain, one arrival per unit; a completed parent's steps run at once
+// (A persistent, software-pipelined variant that deferred every drain and
+// arrival by one block-iteration measured slower: 97.6 vs 74.6 us for n=16,
+// m=5 at 1024 instances, at 207 VGPRs = 2 waves per SIMD.)
+// DIAG (lab only, tools/casc_lab.py, BA_CASC_DIAG; wrong results): 2 = no
+// fan-in (units only), 4 = arrivals but no steps.  The product uses 0.
 template <int N, int ME, int DIAG = 0>
-__global__ __launch_bounds__(256) void k_cascade(CascArgs a) {
+__global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
     using C = Casc<N, ME>;
     constexpr int L = C::L, S = C::S, G = C::G, GP = C::GP, GPW = C::GPW, NIN = C::NIN, Q = C::Q;
     constexpr uint32_t R = C::sz(Q);  // units per word
-    constexpr uint32_t PB = 4u * GPW;
-    constexpr uint32_t NWM = C::nw_max;
     constexpr int NPD = (S + 1) / 2;
     constexpr uint32_t fan = (uint32_t)(L - Q);  // children of a level Q-1 slot (or of the root)
+    using RP = RelayPlan<N, Q + 1, G>;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint64_t* planes = lds;  // [3][NWM][NIN]
+    const uint32_t u0 = blockIdx.x * kCascWaves * GPW;
+    const uint32_t wfirst = u0 / R, nw = (min(u0 + kCascWaves * GPW, a.units) - 1u) / R - wfirst + 1u;
+    uint64_t* planes = lds;  // [nw][NIN]
     uint64_t* tr = lds + C::planes_words + wv * (uint32_t)C::tr_words;
     const uint64_t gw0 = a.first_trial >> 6;
-    const bool staged = a.gs.faulty_mode == 0 && a.gs.order_mode == 0;
-    const uint32_t iters = (a.units + PB - 1) / PB;
-    const uint32_t g = lane / G, x = lane - g * G;
     TrialCounts tc;
-    // the lane's unit of block-iteration `it`
-    auto unit_of = [&](uint32_t it, uint32_t& w, uint32_t& rho) -> bool {
-        const uint32_t u = it * PB + wv * GPW + g;
-        const bool ok = g < (uint32_t)GPW && u < a.units;
-        const uint32_t uu = ok ? u : 0u;
-        w = uu / R;
-        rho = uu - w * R;
-        return ok;
-    };
-    auto first_word = [&](uint32_t it) { return (it * PB) / R; };
-    // pipeline registers
-    constexpr int NSL = C::NSL;
-    WordRegs pf[NSL];
-    static_for<0, NSL>([&](auto i) { pf[i()] = WordRegs{0, 0, false}; });
-    uint64_t pf_mem = 0;
-    auto prefetch = [&](uint32_t it) {
-        const uint32_t wf = first_word(it), wl = (min(it * PB + PB, a.units) - 1u) / R;
-        static_for<0, NSL>([&](auto i) {
-            const uint32_t kw = wv + 4u * i();
-            if (staged && kw <= wl - wf) pf[i()] = load_word(a, wf + kw, lane);
+    const uint32_t g = lane / G, x = lane - g * G;
+    const uint32_t u = u0 + wv * GPW + g;
+    const bool act = g < (uint32_t)GPW && u < a.units;
+    const uint32_t uu = act ? u : u0;
+    const uint32_t w = uu / R, rho = uu - w * R;
+    const uint64_t gw = gw0 + w;
+    const uint32_t sr = rho * (uint32_t)G + x;  // the lane's level me-2 slot
+    const uint32_t gg = act ? g : 0u;
+    uint64_t* xch = tr + gg * (G * GP);  // the unit's relay exchange (before its transpose)
+    // 1. input-free draws
+    uint64_t lw[2 * NPD], mem = 0;
+    const RP rp(rho, rho * (uint32_t)G);
+    if (act) {
+        mem = a.members[sr];
+        lie_pairs<NPD>(a.seed, ME - 1, (sr * (uint32_t)S) >> 1, gw, lw);
+        relay_draw<N, Q + 1, G, G>(a, rp, xch, x, true, gw);
+    }
+    // 2. inputs
+    for (uint32_t k = wv; k < nw; k += kCascWaves)
+        wave_inputs<N, 1, 0>(planes + k * NIN, lane, wfirst + k, a.seed, a.gs, a.first_trial,
+                             a.ntrials, a.faulty, a.order);
+    __syncthreads();
+    // 3. the units (the leaf work sits in a divergent branch: as straight-line
+    //    code for every lane the compiler's schedule needed 256 VGPRs and spilled)
+    const uint64_t* in = planes + (w - wfirst) * NIN;
+    if (act) {
+        uint32_t path[Q + 2], srt[Q + 2];
+        unrank_path<L, Q + 1>(sr, path, srt);
+        const uint64_t par = relay_apply<N, Q + 1, G>(rp, in, xch, x, rho * (uint32_t)G, path);
+        __builtin_amdgcn_wave_barrier();  // xch becomes the transpose below
+        const uint64_t fs = in[path[Q + 1] + 1];  // level me-1 relayer: the slot's last lieutenant
+        const uint64_t oddmask = 0ull - (uint64_t)((sr * (uint32_t)S) & 1u);
+        uint64_t diag[S], Fm[S], Rm[S];
+        static_for<0, S>([&](auto b) {
+            uint64_t lie;
+            if constexpr (S % 2 == 1) lie = lw[b()] ^ ((lw[b()] ^ lw[b() + 1]) & oddmask);
+            else lie = lw[b()];
+            diag[b()] = sel64(fs, lie, par);
+            Fm[b()] = in[(mem >> (5 * b())) & 31u];
         });
-        uint32_t w, rho;
-        if (unit_of(it, w, rho)) pf_mem = a.members[rho * (uint32_t)G + x];
-    };
-    uint32_t it1 = 0xFFFFFFFFu, it2 = 0xFFFFFFFFu;  // iterations of the pending arrivals / steps
-    uint32_t old2 = 0;                              // returned counts of it2's arrivals (x == 0 lanes)
-    // D: the steps of the units of iteration `it` whose arrival returned the last count
-    auto steps = [&](uint32_t it, uint32_t old, uint32_t buf) {
-        uint32_t w, rho;
-        const bool ok = unit_of(it, w, rho);
-        uint64_t m = __ballot(ok && x == 0 && old + 1 == fan);
-        while (m) {  // wave-uniform: every lane runs each completed parent's step
-            const uint32_t b = (uint32_t)__builtin_ctzll(m);
-            m &= m - 1;
-            const uint32_t wb = (uint32_t)__builtin_amdgcn_readlane((int)w, (int)b);
-            const uint32_t rb = (uint32_t)__builtin_amdgcn_readlane((int)rho, (int)b);
-            const uint64_t* inb = planes + (buf * NWM + (wb - first_word(it))) * NIN;
-            casc_step<N, ME, Q>(a, inb, tr, lane, wb, Q >= 1 ? rb / fan : 0u, gw0 + wb, tc);
-        }
-    };
-    // A: one lane per unit adds to the counter of rho's parent (level Q-1), or
-    // at Q = 0 of the word; returns the count before the add
-    auto arrive = [&](uint32_t it) -> uint32_t {
-        uint32_t w, rho, old = 0;
-        if (unit_of(it, w, rho) && x == 0) {
+        leaf_block<S>(ME, a.seed, gw, sr, diag, Fm, Rm);
+        uint64_t* t = tr + (gg * G) * GP + x;
+        t[x * GP] = par;
+        static_for<0, S>([&](auto d) { t[(d() + (d() >= x ? 1u : 0u)) * GP] = Rm[d()]; });
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (act) {
+        const uint64_t* col = tr + (gg * G + x) * GP;
+        Csa<planes_c(G)> cnt;
+        static_for<0, G>([&](auto b) { cnt.template add<b()>(col[b()]); });
+        store_sc1(a.R[ME - 2] + (uint64_t)w * C::sz(ME - 2) + sr, cnt.template ge<G, G / 2 + 1>());
+    }
+    __builtin_amdgcn_wave_barrier();
+    if constexpr ((DIAG & 2) == 0) {
+        drain_stores();
+        // 4. arrivals: one lane per unit at the counter of rho's parent (level
+        //    Q-1) or, at Q = 0, of the word
+        bool last = false;
+        if (act && x == 0) {
             uint32_t* c;
             if constexpr (Q >= 1)
                 c = a.cnt + (uint64_t)(a.cnt_off[Q - 1] + w * C::sz(Q - 1) + rho / fan) * kCascCounterStride;
             else
                 c = a.cnt + (uint64_t)(a.cnt_off[0] + w) * kCascCounterStride;
-            old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (old + 1 == fan) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = old + 1 == fan;
+            if (last) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        return old;
-    };
-    uint32_t k = 0;
-    if (blockIdx.x < iters) prefetch(blockIdx.x);
-    for (uint32_t it = blockIdx.x; it < iters; it += gridDim.x, ++k) {
-        const uint32_t buf = k % 3;
-        const uint32_t wfirst = first_word(it);
-        const uint32_t nw = (min(it * PB + PB, a.units) - 1u) / R - wfirst + 1u;
-        uint64_t* pl = planes + buf * NWM * NIN;
-        // S
-        static_for<0, NSL>([&](auto i) {
-            const uint32_t kw = wv + 4u * i();
-            if (kw < nw) {
-                if (staged) slice_word<N>(pl + kw * NIN, lane, pf[i()]);
-                else wave_inputs<N, 1, 0>(pl + kw * NIN, lane, wfirst + kw, a.seed, a.gs,
-                                          a.first_trial, a.ntrials, a.faulty, a.order);
-            }
-        });
-        const uint64_t mem = pf_mem;
-        __syncthreads();
-        // D
-        if constexpr ((DIAG & 2) == 0) {
-            if (it2 != 0xFFFFFFFFu) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                steps(it2, old2, (k + 1) % 3);  // it2 ran two iterations ago: buffer (k-2) % 3
-            }
-        }
-        // U
-        uint32_t w, rho;
-        const bool act = unit_of(it, w, rho);
-        const uint64_t* in = pl + (w - wfirst) * NIN;
-        const uint64_t gw = gw0 + w;
-        const uint32_t sr = rho * (uint32_t)G + x;  // the lane's level me-2 slot
-        const uint32_t gg = act ? g : 0u;
-        // (the leaf work sits in a divergent branch: as straight-line code for
-        // every lane the compiler's schedule needed 256 VGPRs and spilled)
-        if (act) {
-            uint32_t path[Q + 2], srt[Q + 2];
-            unrank_path<L, Q + 1>(sr, path, srt);
-            // L_{me-2}[rho.x]: the unit's G slots drawn together
-            const uint64_t par = relay_slots<N, Q + 1, G, G>(a, in, tr + gg * (G * GP), x, true, rho,
-                                                              rho * (uint32_t)G, path, gw);
-            const uint64_t fs = in[path[Q + 1] + 1];  // level me-1 relayer: the slot's last lieutenant
-            const uint32_t x0 = sr * (uint32_t)S;
-            uint64_t lw[2 * NPD];
-            lie_pairs<NPD>(a.seed, ME - 1, x0 >> 1, gw, lw);
-            const uint64_t oddmask = 0ull - (uint64_t)(x0 & 1u);
-            uint64_t diag[S], Fm[S], Rm[S];
-            static_for<0, S>([&](auto b) {
-                uint64_t lie;
-                if constexpr (S % 2 == 1) lie = lw[b()] ^ ((lw[b()] ^ lw[b() + 1]) & oddmask);
-                else lie = lw[b()];
-                diag[b()] = sel64(fs, lie, par);
-                Fm[b()] = in[(mem >> (5 * b())) & 31u];
-            });
-            leaf_block<S>(ME, a.seed, gw, sr, diag, Fm, Rm);
-            uint64_t* t = tr + (gg * G) * GP + x;
-            t[x * GP] = par;
-            static_for<0, S>([&](auto d) { t[(d() + (d() >= x ? 1u : 0u)) * GP] = Rm[d()]; });
-        }
-        __builtin_amdgcn_wave_barrier();
-        uint64_t rmaj = 0;
-        if (act) {
-            const uint64_t* col = tr + (gg * G + x) * GP;
-            Csa<planes_c(G)> cnt;
-            static_for<0, G>([&](auto b) { cnt.template add<b()>(col[b()]); });
-            rmaj = cnt.template ge<G, G / 2 + 1>();
-        }
-        __builtin_amdgcn_wave_barrier();
-        // W
-        drain_stores();
-        // P
-        if (it + gridDim.x < iters) prefetch(it + gridDim.x);
-        // A (iteration it1's units; their stores drained above)
-        if constexpr ((DIAG & 2) == 0) {
-            it2 = it1;
-            old2 = it1 != 0xFFFFFFFFu ? arrive(it1) : 0u;
-        }
-        // St
-        if (act) store_sc1(a.R[ME - 2] + (uint64_t)w * C::sz(ME - 2) + sr, rmaj);
-        it1 = it;
-    }
-    if constexpr ((DIAG & 2) == 0) {
-        // pending: the steps of it2 (atomics issued in the last iteration), the
-        // arrivals and steps of it1 (the last iteration)
-        const uint32_t kl = k == 0 ? 0u : k - 1;  // the last iteration's index
-        if (it2 != 0xFFFFFFFFu) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            steps(it2, old2, (kl + 2) % 3);  // it2 = iteration kl - 1
-        }
-        if (it1 != 0xFFFFFFFFu) {
-            drain_stores();
-            const uint32_t o = arrive(it1);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            steps(it1, o, kl % 3);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint64_t lastmask = (DIAG & 4) ? 0ull : __ballot(last);
+        while (lastmask) {  // wave-uniform: every lane runs each completed parent's step
+            const uint32_t b = (uint32_t)__builtin_ctzll(lastmask);
+            lastmask &= lastmask - 1;
+            const uint32_t wb = (uint32_t)__builtin_amdgcn_readlane((int)w, (int)b);
+            const uint32_t rb = (uint32_t)__builtin_amdgcn_readlane((int)rho, (int)b);
+            casc_step<N, ME, Q>(a, planes + (wb - wfirst) * NIN, tr, lane, wb,
+                                Q >= 1 ? rb / fan : 0u, gw0 + wb, tc);
         }
     }
-    wave_flush(tc, lane, wv, 4, a.counters, a.sk, false);
+    wave_flush(tc, lane, wv, kCascWaves, a.counters, a.sk, false);
 }
 
 // ---------------------------------------------------------------------------
@@ -526,21 +443,11 @@ uint64_t cascade_scratch_words_per_word(const Geometry& g) {
 template <int N, int ME, int DIAG = 0>
 static hipError_t launch_cascade_t(CascArgs& ca, uint32_t cu_count, hipStream_t st) {
     using C = Casc<N, ME>;
-    constexpr uint32_t per_block = 4u * C::GPW;
+    constexpr uint32_t per_block = kCascWaves * C::GPW;
     const uint32_t iters = (ca.units + per_block - 1) / per_block;
-    const size_t lds = (size_t)(C::planes_words + 4u * C::tr_words) * sizeof(uint64_t);
-    // persistent: as many blocks as stay resident (block-iterations beyond
-    // that are taken in turn), never more than there are iterations
-    static int occ = 0;
-    if (occ == 0) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_cascade<N, ME, DIAG>, 256, lds) !=
-                hipSuccess ||
-            occ < 1)
-            occ = 1;
-    }
-    const uint32_t resident = (uint32_t)occ * cu_count;
-    const uint32_t blocks = iters < resident ? iters : resident;
-    hipLaunchKernelGGL((k_cascade<N, ME, DIAG>), dim3(blocks ? blocks : 1), dim3(256), lds, st, ca);
+    const size_t lds = (size_t)(C::planes_words + kCascWaves * C::tr_words) * sizeof(uint64_t);
+    const uint32_t blocks = iters;
+    hipLaunchKernelGGL((k_cascade<N, ME, DIAG>), dim3(blocks ? blocks : 1), dim3(64 * kCascWaves), lds, st, ca);
     return hipGetLastError();
 }
 
@@ -580,6 +487,7 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
     if (const char* d = getenv("BA_CASC_DIAG")) {  // lab ablations, n=16 m=5 only
         if (g.n == 16 && g.me == 5) switch (atoi(d)) {
             case 2: return launch_cascade_t<16, 5, 2>(ca, a.cu_count, a.stream);
+            case 4: return launch_cascade_t<16, 5, 4>(ca, a.cu_count, a.stream);
             default: break;
         }
     }

@@ -1100,134 +1100,6 @@ inline hipError_t launch_om3q(const RunArgs& a) {
 }
 
 // ---------------------------------------------------------------------------
-// k_om3s: k_om3w's task split over a block of WAVES = 3 waves (one task =
-// W words x L first-hop rounds).  A k_om3w launch of the bench's 1M trials
-// is 2048 one-task waves, two per SIMD: the SIMD's older wave wins issue
-// arbitration and finishes first, and the younger runs alone for the rest of
-// the launch.  Here a block shares the task's IN | L0 | R1T in LDS, every
-// wave stages and relays level 0 for its WPW words, runs its RPW rounds
-// (om3_round, its own R2T scratch), and takes the roots and the epilogue of
-// its words: 3 x 2048 wave-units of a third of the work each, three per SIMD
-// (163 VGPRs), so the launch ends on a third of a task instead of a whole one.
-// Bit-identical to k_om3w (the same rounds, roots and epilogue).
-// ---------------------------------------------------------------------------
-constexpr int kSplitWaves = 3;
-
-template <int N>
-struct Om3S {
-    static constexpr int L = N - 1, S = N - 3, C = L - 1, CP = C + 1;
-    static constexpr int W = 64 / C, LANES = W * C, NIN = N + 3;
-    static constexpr int WAVES = kSplitWaves;
-    static constexpr int RPW = (L + WAVES - 1) / WAVES;  // rounds per wave
-    static constexpr int WPW = (W + WAVES - 1) / WAVES;  // words per wave (inputs, roots, epilogue)
-    static constexpr int LASTW = W - (WAVES - 1) * WPW;  // the last wave's words (may be <= 0)
-    // shared: IN[W][NIN] | L0[W][L] | R1T[W][L][L]; per wave: R2T[W][C][CP], then A/U [WPW][2L]
-    static constexpr int oIN = 0, oL0 = W * NIN, oR1 = oL0 + W * L;
-    static constexpr int shared = ((oR1 + W * L * L) + 1) & ~1;
-    static constexpr int wave_words = ((W * C * CP > WPW * 2 * L ? W * C * CP : WPW * 2 * L) + 1) & ~1;
-    static constexpr int lds_words = shared + WAVES * wave_words;
-};
-
-// Inputs + level 0 (phase 1) or roots + epilogue (phase 2) of NW words
-// starting at word wb of the task.
-template <int N, int NW, bool STAGED>
-__device__ __forceinline__ void om3s_words(int phase, uint64_t* sh, uint64_t* wimg, uint32_t lane,
-                                           uint32_t wb, uint64_t w0, uint64_t seed, const GenSpec& gs,
-                                           uint64_t first_trial, uint64_t batch,
-                                           const uint32_t* __restrict__ faulty,
-                                           const uint8_t* __restrict__ order,
-                                           uint64_t* __restrict__ decisions,
-                                           uint8_t* __restrict__ outcome, TrialCounts& tc) {
-    if constexpr (NW > 0) {
-        using G = Om3S<N>;
-        constexpr int L = G::L, NIN = G::NIN;
-        uint64_t* in0 = sh + G::oIN + wb * NIN;
-        if (phase == 1) {
-            if constexpr (STAGED) stage_words<N, NW>(in0, lane, w0 + wb, batch, faulty, order);
-            else wave_inputs<N, NW, 0>(in0, lane, w0 + wb, seed, gs, first_trial, batch, faulty, order);
-            __builtin_amdgcn_wave_barrier();
-            level0_r1t<N, NW>(in0, sh + G::oL0 + wb * L, sh + G::oR1 + wb * L * L, lane, seed,
-                              (first_trial >> 6) + w0 + wb);
-        } else {
-            roots_r1t<L, NW>(sh + G::oR1 + wb * L * L, wimg, lane);
-            __builtin_amdgcn_wave_barrier();
-            wave_epilogue<N, NW, 3, 0>(in0, wimg, lane, w0 + wb, batch, decisions, outcome, tc);
-        }
-    }
-}
-
-template <int N, bool STAGED>
-__global__ __launch_bounds__(64 * kSplitWaves, kSplitWaves) void k_om3s(
-    uint64_t seed, GenSpec gs, uint64_t first_trial, uint64_t batch,
-    const uint32_t* __restrict__ faulty, const uint8_t* __restrict__ order,
-    uint64_t* __restrict__ decisions, uint8_t* __restrict__ outcome,
-    uint64_t* __restrict__ counters, Sink sk) {
-    using G = Om3S<N>;
-    constexpr int L = G::L, C = G::C, W = G::W, NIN = G::NIN, RPW = G::RPW, WPW = G::WPW;
-    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint64_t* sh = lds;
-    uint64_t* wimg = lds + G::shared + wv * G::wave_words;
-    const uint64_t total_words = (batch + 63) / 64;
-    const uint64_t ntasks = (total_words + W - 1) / W;
-    const uint32_t lw_ = lane / C, la = lane - lw_ * C;
-    const bool act = lane < (uint32_t)G::LANES;
-    const uint32_t lw = act ? lw_ : 0;
-    const uint32_t wb = wv * WPW;                        // this wave's first word
-    const uint32_t jb = wv * RPW, je = min(jb + RPW, (uint32_t)L);  // this wave's rounds
-    TrialCounts tc;
-    auto words = [&](int phase, uint64_t w0) {
-        if (wv + 1 < (uint32_t)kSplitWaves)
-            om3s_words<N, WPW, STAGED>(phase, sh, wimg, lane, wb, w0, seed, gs, first_trial, batch,
-                                       faulty, order, decisions, outcome, tc);
-        else
-            om3s_words<N, G::LASTW, STAGED>(phase, sh, wimg, lane, wb, w0, seed, gs, first_trial,
-                                            batch, faulty, order, decisions, outcome, tc);
-    };
-    for (uint64_t task = blockIdx.x; task < ntasks; task += gridDim.x) {
-        const uint64_t w0 = task * W;
-        const uint64_t gw = (first_trial >> 6) + w0 + lw;
-        words(1, w0);
-        __syncthreads();
-        const uint64_t* in = sh + G::oIN + lw * NIN;
-        for (uint32_t j1 = jb; j1 < je; ++j1) {
-            const uint64_t r1 = om3_round<N>(in, act ? sh[G::oL0 + lw * L + j1] : 0ull, wimg, lw, la,
-                                             act, j1, seed, gw);
-            if (act) sh[G::oR1 + (lw * L + la + (la >= j1 ? 1u : 0u)) * L + j1] = r1;
-        }
-        __syncthreads();
-        words(2, w0);
-        __syncthreads();  // IN, L0 and R1T are the next task's
-    }
-    block_flush<kSplitWaves>(tc, lane, wv, counters, sk);
-}
-
-template <int N>
-inline hipError_t launch_om3s(const RunArgs& a) {
-    using G = Om3S<N>;
-    const uint64_t words = (a.batch + 63) / 64, tasks = (words + G::W - 1) / G::W;
-    // persistent: four 3-wave blocks per CU (three waves per SIMD)
-    uint64_t blocks = 4ull * a.cu_count;
-    if (const char* e = getenv("BA_WAVE_MAX_BLOCKS")) {  // tests: force the persistent task loop
-        const uint64_t c = strtoull(e, nullptr, 0);
-        if (c >= 1 && c < blocks) blocks = c;
-    }
-    if (blocks > tasks) blocks = tasks;
-    if (blocks < 1) blocks = 1;
-    const size_t lds = (size_t)G::lds_words * 8;
-    ProfScope ps(a.prof, "k_om3s", a.stream);
-    if (a.gen.faulty_mode == 0 && a.gen.order_mode == 0)
-        hipLaunchKernelGGL((k_om3s<N, true>), dim3((uint32_t)blocks), dim3(64 * kSplitWaves), lds,
-                           a.stream, a.seed, a.gen, a.first_trial, a.batch, a.faulty, a.order,
-                           a.decisions, a.outcome, a.counters, a.sink);
-    else
-        hipLaunchKernelGGL((k_om3s<N, false>), dim3((uint32_t)blocks), dim3(64 * kSplitWaves), lds,
-                           a.stream, a.seed, a.gen, a.first_trial, a.batch, a.faulty, a.order,
-                           a.decisions, a.outcome, a.counters, a.sink);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
 // k_om4w: effective depth 4 (n=13, m=4 is SURVEY config 3).  Same wave-task
 // design one level deeper: a round is a second-level subtree (j1, j2), whose
 // C2 = L-2 level-2 slots (j1, j2, a) are C2 leaf blocks, so lane (w, a),

@@ -17,7 +17,6 @@ hipError_t launch_wave_engine(const RunArgs& a, const Geometry& g) {
     // depth 3: k_om3w; BA_WAVE_KIND=2 selects the block-queue kernel k_om3q (A/B,
     // cross-checks: DESIGN.md §4 on why the queue did not pay)
     const char* kind = getenv("BA_WAVE_KIND");
-    if (kind && kind[0] == '3' && g.n == 10) return launch_om3s<10>(a);  // lab A/B (k_om3s)
     if (kind && kind[0] == '2') {
         switch (g.n) {
 #define OM3Q_CASE(nn) \

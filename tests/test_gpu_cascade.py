@@ -83,27 +83,3 @@ def test_cascade_equals_multi_launch_pipeline(engine, monkeypatch, n, m, B):
         same(r.outcome, a.outcome, "outcome")
         assert r.counters == a.counters
 
-
-@pytest.mark.parametrize("B,blocks", [(1 << 20, None), (64 * 8 * 37 + 5, None), (64 * 8 * 37 + 5, 3)])
-@pytest.mark.parametrize("staged", [True, False])
-def test_split_wave_kernel_equals_k_om3w(engine, monkeypatch, B, blocks, staged):
-    """k_om3s (BA_WAVE_KIND=3: k_om3w's task split over a block of three waves)
-    gives k_om3w's bits at n=10, m=3: the bench's 1M trials, a ragged batch, and
-    the persistent task loop (BA_WAVE_MAX_BLOCKS=3); staged or drawn inputs."""
-    from ba_amd import lib as L
-    kw = dict(seed=0xBA5EED, f=3, first_trial=64 * 8 * 5)
-    if staged:
-        rng = np.random.default_rng(B)
-        fm = (rng.integers(0, 1 << 10, B) & rng.integers(0, 1 << 10, B) &
-              rng.integers(0, 1 << 10, B)).astype(np.uint32)
-        kw.update(faulty=fm, order=rng.integers(0, 3, B).astype(np.uint8))
-    else:
-        kw.update(faulty_mode=L.FAULTY_RANDOM, order_mode=L.ORDER_RANDOM)
-    a = engine.run(10, 3, B, **kw)
-    monkeypatch.setenv("BA_WAVE_KIND", "3")
-    if blocks:
-        monkeypatch.setenv("BA_WAVE_MAX_BLOCKS", str(blocks))
-    b = engine.run(10, 3, B, **kw)
-    same(b.decisions, a.decisions, "decisions")
-    same(b.outcome, a.outcome, "outcome")
-    assert b.counters == a.counters

@@ -2,7 +2,7 @@
 ablated results are wrong by design).  One JSON line per (batch, diag):
 average time per call of `reps` calls back to back on one stream.
 
-    python tools/casc_lab.py [--batches 1,1024] [--diags 0,2]
+    python tools/casc_lab.py [--batches 1,1024] [--diags 0,2,4]
 """
 from __future__ import annotations
 
@@ -22,7 +22,7 @@ from ba_amd import lib as L  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batches", default="1,1024")
-    ap.add_argument("--diags", default="0,2")
+    ap.add_argument("--diags", default="0,2,4")
     ap.add_argument("--reps", type=int, default=100)
     ap.add_argument("--n", type=int, default=16)
     ap.add_argument("--m", type=int, default=5)
