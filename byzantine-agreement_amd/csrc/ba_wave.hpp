@@ -746,7 +746,9 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
 }
 
 // ---------------------------------------------------------------------------
-// k_om3q: effective depth 3 with a block-level work queue (the bench kernel).
+// k_om3q: effective depth 3 with a block-level work queue (A/B only:
+// BA_WAVE_KIND=2; k_om3w is the bench kernel, DESIGN.md §4 on why the queue
+// did not pay).
 //
 // k_om3w gives each wave a whole task (W words x all L first-hop rounds).  At
 // two waves per SIMD the SIMD's older wave wins VALU arbitration, finishes its

@@ -4,7 +4,10 @@ this job's host threads) -- not sampled.
 
   config 2  n=10, m=3: all 1,048,576 trials of the bench's first step stream
             (seed 0xBA5EED, f ~ U{0..3}, random orders), staged and in-kernel inputs
-  config 3  n=13, m=4: 65,536 trials (f ~ U{0..4})
+  config 3  n=13, m=4: 65,536 trials (f ~ U{0..4}) vs the textbook oracle, and
+            2,097,152 trials vs the word-sliced C port (itself pinned on the oracle)
+  config 4  n=10, m=3 sweep f = 0..4 exactly faulty, the committed curve's 1,048,576
+            trials per point (tools/run_configs.py's trial ranges) vs the sliced port
   config 5  n=16, m=5: the full batch of 1024 instances, unsplit and through the
             first-hop split (world 1), plus the word-sliced C port as a second check
 
@@ -71,6 +74,33 @@ def test_config3_65536_trials_vs_oracle(engine):
     check(res.decisions, res.outcome, res.counters, od, oo, ocnt, "config 3 (auto engine)")
     sd, so, sc = oracle_c.sliced_run(13, 4, B, threads=host_threads(), **kw)
     check(sd, so, sc, od, oo, ocnt, "C port vs oracle")
+
+
+def test_config3_2m_trials_vs_sliced_port(engine):
+    from ba_amd import lib as L
+    B = 1 << 21
+    kw = dict(seed=0xBA5EED, faulty_mode=L.FAULTY_RANDOM, f=4, order_mode=L.ORDER_RANDOM,
+              first_trial=1 << 22)
+    sd, so, sc = oracle_c.sliced_run(13, 4, B, threads=host_threads(), **kw)
+    assert sc["trials"] == B
+    res = engine.run(13, 4, B, **kw)
+    check(res.decisions, res.outcome, res.counters, sd, so, sc, "config 3, 2M trials")
+
+
+def test_config4_curve_1m_per_point_vs_sliced_port(engine):
+    """The f-sweep of tools/run_configs.py (exactly f faulty, point f on trials
+    [f*T, (f+1)*T)) at its committed size, T = 1,048,576 per point."""
+    from ba_amd import lib as L
+    T = 1 << 20
+    for f in range(0, 5):
+        kw = dict(seed=0xBA5EED, faulty_mode=L.FAULTY_EXACT, f=f, order_mode=L.ORDER_RANDOM,
+                  first_trial=T * f)
+        sd, so, sc = oracle_c.sliced_run(10, 3, T, threads=host_threads(), **kw)
+        res = engine.run(10, 3, T, **kw)
+        check(res.decisions, res.outcome, res.counters, sd, so, sc, f"config 4, f={f}")
+        assert sc["faulty_total"] == f * T
+        if f <= 3:
+            assert sc["bound_violations"] == 0 and sc["agreement"] == T
 
 
 def test_config5_full_batch_vs_oracle(engine):
