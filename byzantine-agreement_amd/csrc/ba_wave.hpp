@@ -453,6 +453,35 @@ __device__ __forceinline__ void wave_epilogue(uint64_t* in0, const uint64_t* au0
     }
 }
 
+// Wave sums of one task's run counters added into `mine` (lane c holds
+// counter c).  Folding after every task keeps the C_NUM per-lane counters live
+// only across the epilogue, not across the task's rounds (12 VGPRs).
+__device__ __forceinline__ void wave_fold(const TrialCounts& tc, uint32_t lane, uint64_t& mine) {
+#pragma unroll
+    for (int c = 0; c < C_NUM; ++c) {
+        uint32_t x = tc.v[c];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+        if (lane == (uint32_t)c) mine += x;
+    }
+}
+
+// Run counters of the block from the waves' folded sums: the waves combine in
+// LDS, then one sink unit per block.  Every wave of the block must call it (it
+// contains a block barrier).
+__device__ __forceinline__ void wave_flush_folded(uint64_t mine, uint32_t lane, uint32_t wv,
+                                                  uint32_t wpb, uint64_t* __restrict__ counters,
+                                                  const Sink& sk, bool skip) {
+    __shared__ unsigned long long wcnt[kWaveThreads / 64][16];
+    if (lane < 16) wcnt[wv][lane] = mine;
+    __syncthreads();
+    if (wv == 0 && !skip) {
+        uint64_t tot = 0;
+        for (uint32_t k = 0; k < wpb; ++k) tot += lane < 16 ? wcnt[k][lane] : 0;
+        sink_counters(lane, tot, blockIdx.x, gridDim.x, counters, sk);
+    }
+}
+
 // Run counters of the block: wave sums (lane c holds counter c), the waves
 // combine in LDS, then one sink unit per block.  Every wave of the block
 // must call it (it contains a block barrier).
@@ -498,31 +527,97 @@ __device__ __forceinline__ void wave_alternate_priority(uint32_t round) {
 // Every lane of the wave calls it (it holds a wave barrier); lanes with !act
 // return 0.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ P4 sel_p4(bool c, const P4& a, const P4& b) {
+    return P4{c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w};
+}
+
 // The value of lane ^ 1 (DPP quad_perm [1,0,3,2]: a VALU move, where
 // __shfl_xor goes through ds_bpermute and waits out an LDS round trip).
 __device__ __forceinline__ uint32_t swap_pair(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
 }
 
+// Per-lane byte offsets (EROW mode of om3_round): K small offsets packed one
+// per byte, fixed per lane for the whole kernel.  Addresses built from them
+// inside the round (one byte-select add each) replace K loop-invariant address
+// VGPRs that the compiler would otherwise hoist out of the round loop.
+template <int K>
+struct LaneBytes {
+    static constexpr int NB = (K + 7) / 8;
+    uint64_t b[NB];
+    template <typename F>
+    __device__ __forceinline__ explicit LaneBytes(F f) {
+        static_for<0, NB>([&](auto k) { b[k()] = 0; });
+        static_for<0, K>([&](auto i) { b[i() / 8] |= (uint64_t)(f(i()) & 0xffu) << (8 * (i() % 8)); });
+    }
+    template <int I>
+    __device__ __forceinline__ uint32_t get() const {
+        return (uint32_t)(b[I / 8] >> (8 * (I % 8))) & 0xffu;
+    }
+};
+
+__device__ __forceinline__ void opaque_v(uint64_t& x) { asm volatile("" : "+v"(x)); }
+
+// The two tables of lane (lw, la) in the depth-3 rounds (n <= 14: every
+// offset < 256):
+//   mem[a] = 8 (a + (a >= la)): member a's word in the E row (below)
+//   r2t[d] = 8 (C + 1) (d >= la): member d's R2T row is d + (d >= la); the
+//            8 (C + 1) d part is the store's immediate offset
 template <int N>
+struct Om3LaneOffsets {
+    static constexpr int S = N - 3, CP = N - 1;
+    LaneBytes<S> mem, r2t;
+    __device__ __forceinline__ explicit Om3LaneOffsets(uint32_t la)
+        : mem([la](int a) { return 8u * (a + ((uint32_t)a >= la ? 1u : 0u)); }),
+          r2t([la](int d) { return (uint32_t)d >= la ? 8u * CP : 0u; }) {}
+    // a copy the compiler cannot see through, taken once per round
+    __device__ __forceinline__ Om3LaneOffsets round_copy() const {
+        Om3LaneOffsets o = *this;
+        static_for<0, LaneBytes<S>::NB>([&](auto k) {
+            opaque_v(o.mem.b[k()]);
+            opaque_v(o.r2t.b[k()]);
+        });
+        return o;
+    }
+};
+
+// EROW = true (k_om3w, rounds in order j1 = 0, 1, ...): the members' faulty
+// words come from the word's E row (erow: E[lw][0..C], E[C] a spare slot):
+// E = the lieutenants other than j1 in rank order, which moves by ONE entry per
+// round (E[j1] becomes lieutenant j1's word for round j1 + 1: the lanes with
+// la == j1 write it, after this round's reads).  One byte extract + add per
+// member instead of two rank compares, selects and shifts.  EROW = false
+// (k_om3q: rounds in any order) ranks the members from j1 and j2 each round.
+template <int N, bool EROW = false>
 __device__ __forceinline__ uint64_t om3_round(const uint64_t* in, uint64_t l0j1, uint64_t* r2t_w,
                                               uint32_t lw, uint32_t la, bool act, uint32_t j1,
-                                              uint64_t seed, uint64_t gw) {
+                                              uint64_t seed, uint64_t gw,
+                                              uint64_t* erow = nullptr,
+                                              const Om3LaneOffsets<N>* lo_ = nullptr) {
     constexpr int L = N - 1, S = N - 3, C = L - 1, CP = C + 1;
     constexpr uint32_t ME = 3;
     const uint32_t sr = j1 * C + la;             // level-1 slot (j1, j2)
     const uint32_t j2 = la + (la >= j1);
+    Om3LaneOffsets<N> ofs(0u);
+    if constexpr (EROW) ofs = lo_->round_copy();
     if (act) {
         // the round's input planes, loaded before the Philox group so their
         // LDS latency hides under it: F[j1] (level-1 sender), F[j2] (level-2
         // sender) and the faulty words of the block's S members
-        const uint32_t lo = j1 < j2 ? j1 : j2, hi = j1 < j2 ? j2 : j1;
         const uint64_t fj = in[j1 + 1], fs = in[j2 + 1];
         uint64_t Fm[S];
-        static_for<0, S>([&](auto a) {
-            const uint32_t ida = a() + (a() >= lo) + (a() + 1 >= hi);  // member a's rank
-            Fm[a()] = in[ida + 1];
-        });
+        if constexpr (EROW) {
+            const char* eb = (const char*)erow;
+            static_for<0, S>([&](auto a) {
+                Fm[a()] = *(const uint64_t*)(eb + ofs.mem.template get<a()>());
+            });
+        } else {
+            const uint32_t lo = j1 < j2 ? j1 : j2, hi = j1 < j2 ? j2 : j1;
+            static_for<0, S>([&](auto a) {
+                const uint32_t ida = a() + (a() >= lo) + (a() + 1 >= hi);  // member a's rank
+                Fm[a()] = in[ida + 1];
+            });
+        }
         // 1. L1[j1, a] (sender j1 relays L0[j1]) and the level-2 diagonal
         //    pairs of leaf block (j1, a): one interleaved Philox group
         const uint32_t x0 = sr * S;
@@ -545,14 +640,17 @@ __device__ __forceinline__ uint64_t om3_round(const uint64_t* in, uint64_t l0j1,
             });
             philox10_n<NPD>(pc, (uint32_t)seed, (uint32_t)(seed >> 32));
             // even lane sends its level-1 pair, odd lane its first level-2 pair
-            P4 snd = odd ? pc[0] : pc[NPD - 1], rcv;
+            // (component-wise selects: a select of whole P4 values can become a
+            // dynamically indexed scratch array)
+            const P4 snd = sel_p4(odd, pc[0], pc[NPD - 1]);
+            P4 rcv;
             rcv.x = swap_pair(snd.x);
             rcv.y = swap_pair(snd.y);
             rcv.z = swap_pair(snd.z);
             rcv.w = swap_pair(snd.w);
-            const P4 p1 = odd ? rcv : pc[NPD - 1];
+            const P4 p1 = sel_p4(odd, rcv, pc[NPD - 1]);
             static_for<0, NPD>([&](auto qd) {
-                const P4 q = (qd() == NPD - 1 && !odd) ? rcv : pc[qd()];
+                const P4 q = qd() == NPD - 1 ? sel_p4(odd, pc[qd()], rcv) : pc[qd()];
                 lw2[2 * qd()] = (uint64_t)q.y << 32 | q.x;
                 lw2[2 * qd() + 1] = (uint64_t)q.w << 32 | q.z;
             });
@@ -585,7 +683,14 @@ __device__ __forceinline__ uint64_t om3_round(const uint64_t* in, uint64_t l0j1,
         // receiver-major: member d of block a is receiver b = d + (d >= a)
         uint64_t* r2t = r2t_w + lw * C * CP + la;
         r2t[la * CP] = par;
-        static_for<0, S>([&](auto d) { r2t[(d() + (d() >= la ? 1u : 0u)) * CP] = R[d()]; });
+        if constexpr (EROW) {
+            char* rb = (char*)r2t;
+            static_for<0, S>([&](auto d) {
+                *(uint64_t*)(rb + ofs.r2t.template get<d()>() + 8 * CP * d()) = R[d()];
+            });
+        } else {
+            static_for<0, S>([&](auto d) { r2t[(d() + (d() >= la ? 1u : 0u)) * CP] = R[d()]; });
+        }
     }
     __builtin_amdgcn_wave_barrier();
     uint64_t r1 = 0;
@@ -601,6 +706,10 @@ __device__ __forceinline__ uint64_t om3_round(const uint64_t* in, uint64_t l0j1,
         Csa<planes_c(C)> cnt;
         static_for<0, C>([&](auto a) { cnt.template add<a()>(cv[a()]); });
         r1 = cnt.template ge<C, C / 2 + 1>();  // inner tie -> non-attack
+        // E for round j1 + 1: E[j1] = lieutenant j1's word (this round's E reads
+        // were issued above, and one wave's LDS operations complete in order);
+        // the other lanes store to the row's spare slot E[C], so no branch
+        if constexpr (EROW) erow[la == j1 ? la : (uint32_t)C] = in[j1 + 1];
     }
     __builtin_amdgcn_wave_barrier();  // r2t is rewritten by the next round
     return r1;
@@ -619,7 +728,8 @@ struct Om3W {
     // IN[W][NIN] | L0[W][L] | R2T[W][C][CP] | R1T[W][L][L] (root inputs, receiver-major:
     // R1T[w][j2][j1] = R1[j1, j2], L0[j2] on the diagonal) ; A/U roots reuse R2T
     static constexpr int oIN = 0, oL0 = oIN + W * NIN, oR2 = oL0 + W * L, oR1 = oR2 + W * C * CP;
-    static constexpr int end0 = oR1 + W * L * L;
+    static constexpr int oE = oR1 + W * L * L;     // E[W][C + 1] (om3_round EROW mode)
+    static constexpr int end0 = oE + W * (C + 1);
     static constexpr bool au_in_r2 = 2 * L <= C * CP;
     static constexpr int oAU = au_in_r2 ? oR2 : end0;
     static constexpr int words = ((au_in_r2 ? end0 : end0 + W * 2 * L) + 1) & ~1;
@@ -687,7 +797,8 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
     const uint32_t lw_ = lane / C, la = lane - lw_ * C;
     const bool act = lane < (uint32_t)G::LANES;
     const uint32_t lw = act ? lw_ : 0;
-    TrialCounts tc;
+    const Om3LaneOffsets<N> lofs(la);
+    uint64_t folded = 0;  // run counters folded per task (wave_fold)
     FUSED_STAMP_INIT();
 #ifdef BA_FUSED_STAMPS
     const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
@@ -706,16 +817,20 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
         __builtin_amdgcn_wave_barrier();
         FUSED_STAMP(0);
         level0_r1t<N, W>(img + G::oIN, img + G::oL0, img + G::oR1, lane, seed, gw0);
+        // E row of round 0: lieutenants 1 .. L-1 (general g's word is in[g])
+        const uint64_t* in = img + G::oIN + lw * NIN;
+        uint64_t* erow = img + G::oE + lw * (C + 1);
+        if (act) erow[la] = in[la + 2];
         __builtin_amdgcn_wave_barrier();
         // ---- subtree rounds ------------------------------------------------------
-        const uint64_t* in = img + G::oIN + lw * NIN;
         const uint64_t gw = gw0 + lw;
         for (uint32_t j1 = 0; j1 < (uint32_t)L; ++j1) {
             // lab only: alternate the issue priority of the SIMD's two waves every
             // round (round 1 default; round 2 measured it 2.5 us slower, om3_lab)
             if constexpr ((DIAG & 8) != 0) wave_alternate_priority(j1);
-            const uint64_t r1 = om3_round<N>(in, act ? img[G::oL0 + lw * L + j1] : 0ull,
-                                             img + G::oR2, lw, la, act, j1, seed, gw);
+            const uint64_t r1 = om3_round<N, true>(in, act ? img[G::oL0 + lw * L + j1] : 0ull,
+                                                   img + G::oR2, lw, la, act, j1, seed, gw,
+                                                   erow, &lofs);
             FUSED_STAMP(1);
             // R1[j1, b] is root input j1 of receiver column j2(b)
             if (act) img[G::oR1 + (lw * L + la + (la >= j1 ? 1u : 0u)) * L + j1] = r1;
@@ -725,12 +840,16 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
         roots_r1t<L, W>(img + G::oR1, img + G::oAU, lane);
         __builtin_amdgcn_wave_barrier();
         FUSED_STAMP(3);
-        wave_epilogue<N, W, ME, DIAG>(img + G::oIN, img + G::oAU, lane, w0, batch, decisions,
-                                      outcome, tc);
+        {
+            TrialCounts tc;
+            wave_epilogue<N, W, ME, DIAG>(img + G::oIN, img + G::oAU, lane, w0, batch, decisions,
+                                          outcome, tc);
+            wave_fold(tc, lane, folded);
+        }
         __builtin_amdgcn_wave_barrier();
         FUSED_STAMP(4);
     }
-    wave_flush(tc, lane, wv, wpb, counters, sk, (DIAG & 4) != 0);
+    wave_flush_folded(folded, lane, wv, wpb, counters, sk, (DIAG & 4) != 0);
 #ifdef BA_FUSED_STAMPS
     if (lane == 0 && blockIdx.x * wpb + wv < (uint32_t)kPartialRows)
     {
@@ -1127,7 +1246,8 @@ struct Om4W {
     static constexpr int NIN = N + 3;
     static constexpr int oIN = 0, oL0 = oIN + W * NIN, oR3 = oL0 + W * L;
     static constexpr int oR1 = oR3 + W * C2 * C2, oRC = oR1 + W * C1 * P1;
-    static constexpr int end0 = oRC + W * L * P;
+    static constexpr int oE = oRC + W * L * P;   // E2[W][C2 + 1] (members, see k_om4w)
+    static constexpr int end0 = oE + W * (C2 + 1);
     static constexpr bool au_in_r3 = 2 * L <= C2 * C2;
     static constexpr int oAU = au_in_r3 ? oR3 : end0;
     static constexpr int words = ((au_in_r3 ? end0 : end0 + W * 2 * L) + 1) & ~1;
@@ -1151,7 +1271,11 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om4w(
     const uint32_t lw_ = lane / C2, la = lane - lw_ * C2;
     const bool act = lane < (uint32_t)G::LANES;
     const uint32_t lw = act ? lw_ : 0;
-    TrialCounts tc;
+    // member a of lane la's leaf block is E2[a + (a >= la)]; member d's R3T row
+    // is d + (d >= la) (the k_om3w tables, E2 in place of E, C2 in place of C + 1)
+    const LaneBytes<S> mem([la](int a) { return 8u * (a + ((uint32_t)a >= la ? 1u : 0u)); });
+    const LaneBytes<S> r3o([la](int d) { return (uint32_t)d >= la ? 8u * C2 : 0u; });
+    uint64_t folded = 0;  // run counters folded per task (wave_fold)
     // tasks: the first wave-round static, then (sk.tasks != nullptr: a persistent
     // launch) each further task from the launch's atomic counter, fetched at the
     // start of the current task so its latency hides behind the task: a wave
@@ -1169,11 +1293,20 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om4w(
         wave_level0<N, W, P>(img + G::oIN, img + G::oL0, img + G::oRC, lane, seed, gw0);
         __builtin_amdgcn_wave_barrier();
         const uint64_t* in = img + G::oIN + lw * NIN;
+        uint64_t* erow = img + G::oE + lw * (C2 + 1);
         const uint64_t gw = gw0 + lw;
         uint32_t round = 0;
         for (uint32_t j1 = 0; j1 < (uint32_t)L; ++j1) {
             // R1 counters of this j1 start at zero
             for (uint32_t it = lane; it < (uint32_t)(W * C1 * P1); it += 64) img[G::oR1 + it] = 0;
+            // E2 of round (j1, c2 = 0): the lieutenants other than j1 and j2 = the
+            // first non-j1, ascending, i.e. non-j1 ranks 1 .. C1-1 (a faulty word of
+            // lieutenant j sits at in[j + 1]).  Each round c2 then moves E2 by one
+            // entry: E2[c2] becomes j2(c2)'s word (below).
+            if (act) {
+                const uint32_t r = la + 1;
+                erow[la] = in[r + (r >= j1 ? 1u : 0u) + 1];
+            }
             __builtin_amdgcn_wave_barrier();
             const uint64_t fj1 = in[j1 + 1];
             const uint64_t l0j1 = img[G::oL0 + lw * L + j1];
@@ -1183,11 +1316,18 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om4w(
                 // as k_om3w's R2T: 0.6% slower)
                 wave_alternate_priority(round);
                 const uint32_t j2 = c2 + (c2 >= j1);
-                const uint32_t lo = j1 < j2 ? j1 : j2, hi = j1 < j2 ? j2 : j1;
                 const uint32_t x1 = j1 * C1 + c2;     // level-1 slot (j1, j2)
                 const uint32_t x2 = x1 * C2 + la;     // level-2 slot (j1, j2, j3): leaf block
-                const uint32_t j3 = la + (la >= lo) + (la + 1 >= hi);  // the a-th other lieutenant
+                // j3 = E2[la] (the la-th lieutenant other than j1, j2); its rank
+                // among the non-j1 lieutenants is la + (la >= c2)
                 uint64_t par = 0, l1v = 0;
+                // the byte tables pass through an empty asm each round, so their
+                // addresses are formed here, not hoisted into 2S live VGPRs
+                LaneBytes<S> memr = mem, r3r = r3o;
+                static_for<0, LaneBytes<S>::NB>([&](auto k) {
+                    opaque_v(memr.b[k()]);
+                    opaque_v(r3r.b[k()]);
+                });
                 if (act) {
                     const uint32_t x3 = x2 * S;
                     constexpr int NPD = (S + 1) / 2;
@@ -1211,28 +1351,25 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om4w(
                     const uint64_t fj2 = in[j2 + 1];
                     par = (fj2 & lie2) | (~fj2 & l1v);               // L2[j1, j2, j3], sender j2
                     // members of leaf block (j1, j2, j3): the lieutenants not in
-                    // {j1, j2, j3}, ascending
-                    const uint32_t e0 = lo < j3 ? lo : j3;
-                    const uint32_t e2 = hi > j3 ? hi : j3;
-                    const uint32_t e1 = lo + hi + j3 - e0 - e2;
-                    const uint64_t fs = in[j3 + 1];  // level-3 sender: j3
+                    // {j1, j2, j3}, ascending = E2 without its entry la
+                    const uint64_t fs = erow[la];  // level-3 sender: j3
                     const uint64_t oddmask = 0ull - (uint64_t)(x3 & 1u);
+                    const char* eb = (const char*)erow;
                     uint64_t diag[S], Fm[S], R[S];
                     static_for<0, S>([&](auto d) {
                         uint64_t lie3;
                         if constexpr (S % 2 == 1) lie3 = lw3[d()] ^ ((lw3[d()] ^ lw3[d() + 1]) & oddmask);
                         else lie3 = lw3[d()];
                         diag[d()] = (fs & lie3) | (~fs & par);
-                        uint32_t m = d();
-                        m += m >= e0 ? 1u : 0u;
-                        m += m >= e1 ? 1u : 0u;
-                        m += m >= e2 ? 1u : 0u;
-                        Fm[d()] = in[m + 1];
+                        Fm[d()] = *(const uint64_t*)(eb + memr.template get<d()>());
                     });
                     leaf_block<S>(ME, seed, gw, x2, diag, Fm, R);
                     uint64_t* r3t = img + G::oR3 + lw * C2 * C2 + la;
                     r3t[la * C2] = par;
-                    static_for<0, S>([&](auto d) { r3t[(d() + (d() >= la ? 1u : 0u)) * C2] = R[d()]; });
+                    char* rb = (char*)r3t;
+                    static_for<0, S>([&](auto d) {
+                        *(uint64_t*)(rb + r3r.template get<d()>() + 8 * C2 * d()) = R[d()];
+                    });
                 }
                 __builtin_amdgcn_wave_barrier();
                 if (act) {
@@ -1241,8 +1378,12 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om4w(
                     Csa<planes_c(C2)> cnt;
                     static_for<0, C2>([&](auto a) { cnt.template add<a()>(col[a()]); });
                     const uint64_t r2 = cnt.template ge<C2, C2 / 2 + 1>();  // inner tie -> non-attack
-                    // receiver j3 (same formula as above) as a rank among the non-j1
-                    planes_add<P1>(img + G::oR1 + (lw * C1 + (j3 - (j3 > j1 ? 1u : 0u))) * P1, r2);
+                    // receiver j3 as a rank among the non-j1 lieutenants
+                    planes_add<P1>(img + G::oR1 + (lw * C1 + la + (la >= c2 ? 1u : 0u)) * P1, r2);
+                    // E2 for round c2 + 1: E2[c2] = j2's word (this round's E2 reads
+                    // were issued above, and one wave's LDS operations complete in
+                    // order); the other lanes store to the spare slot E2[C2]
+                    erow[la == c2 ? la : (uint32_t)C2] = in[j2 + 1];
                 }
                 __builtin_amdgcn_wave_barrier();
                 if (act && la == 0) planes_add<P1>(img + G::oR1 + (lw * C1 + c2) * P1, l1v);
@@ -1261,11 +1402,15 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om4w(
         }
         wave_roots<L, W, P>(img + G::oRC, img + G::oAU, lane);
         __builtin_amdgcn_wave_barrier();
-        wave_epilogue<N, W, ME, 0>(img + G::oIN, img + G::oAU, lane, w0, batch, decisions, outcome, tc);
+        {
+            TrialCounts tc;
+            wave_epilogue<N, W, ME, 0>(img + G::oIN, img + G::oAU, lane, w0, batch, decisions, outcome, tc);
+            wave_fold(tc, lane, folded);
+        }
         __builtin_amdgcn_wave_barrier();
         task = sk.tasks != nullptr ? nwaves + __builtin_amdgcn_readfirstlane(next_raw) : task + nwaves;
     }
-    wave_flush(tc, lane, wv, wpb, counters, sk, false);
+    wave_flush_folded(folded, lane, wv, wpb, counters, sk, false);
 }
 
 // WAVE engine launch: one wave per W-word task, 4 independent waves per block,
