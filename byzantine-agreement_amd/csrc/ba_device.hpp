@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <type_traits>
+#include "ba_philox_asm.hpp"
 
 namespace ba {
 
@@ -178,6 +179,45 @@ __host__ __device__ __forceinline__ void philox10_n(P4 (&c)[G], uint32_t k0, uin
     k0 = as_vgpr(k0);
     k1 = as_vgpr(k1);
 #endif
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(BA_PHILOX_C) && !defined(BA_PHILOX_ROUND_ASM)
+    // rounds 0-1 in C (the compiler shares and strength-reduces the products a
+    // lane's calls have in common), rounds 2-9 as one asm statement
+    // (ba_philox_asm.hpp: one hazard s_nop per group instead of one per round)
+    if constexpr (G >= 2 && G <= 4) {
+        static_for_h<0, 2>([&](auto i) {
+            uint64_t p0[G], p1[G];
+            philox_mul2_n<i(), G>(c, p0, p1);
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                P4 n;
+                n.x = xor3_32((uint32_t)(p1[g] >> 32), c[g].y, k0);
+                n.y = (uint32_t)p1[g];
+                n.z = xor3_32((uint32_t)(p0[g] >> 32), c[g].w, k1);
+                n.w = (uint32_t)p0[g];
+                c[g] = n;
+            }
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        });
+        uint32_t rk0[8], rk1[8], x[G], y[G], z[G], w[G];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            rk0[i] = k0 + (uint32_t)i * 0x9E3779B9u;
+            rk1[i] = k1 + (uint32_t)i * 0xBB67AE85u;
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            x[g] = c[g].x;
+            y[g] = c[g].y;
+            z[g] = c[g].z;
+            w[g] = c[g].w;
+        }
+        philox_r29_asm<G>(x, y, z, w, rk0, rk1);
+#pragma unroll
+        for (int g = 0; g < G; ++g) c[g] = P4{x[g], y[g], z[g], w[g]};
+        return;
+    }
+#endif
     static_for_h<0, 10>([&](auto i) {
         uint64_t p0[G], p1[G];
         philox_mul2_n<i(), G>(c, p0, p1);
@@ -193,6 +233,20 @@ __host__ __device__ __forceinline__ void philox10_n(P4 (&c)[G], uint32_t k0, uin
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
     });
+}
+
+// G calls as consecutive groups of at most 4 interleaved calls (sizes as even as
+// possible: 7 -> 4 + 3), so no more than four calls' state is live at once.
+template <int G, int B = 0>
+__host__ __device__ __forceinline__ void philox_groups(P4 (&c)[G], uint32_t k0, uint32_t k1) {
+    if constexpr (B < G) {
+        constexpr int left = G - B, ngrp = (left + 3) / 4, g = (left + ngrp - 1) / ngrp;
+        P4 sub[g];
+        static_for_h<0, g>([&](auto i) { sub[i()] = c[B + i()]; });
+        philox10_n<g>(sub, k0, k1);
+        static_for_h<0, g>([&](auto i) { c[B + i()] = sub[i()]; });
+        philox_groups<G, B + g>(c, k0, k1);
+    }
 }
 
 // Lie words of slots 2*pair and 2*pair+1 at level k for global trial word gw.

@@ -31,10 +31,90 @@ constexpr int leaf_philox_group(int npair) { return npair % BA_LEAF_PG == 0 ? BA
 constexpr int leaf_philox_group(int npair) { return npair % 3 == 0 ? 3 : (npair % 4 == 0 ? 4 : (npair % 2 == 0 ? 2 : 3)); }
 #endif
 
+// Column-ordered schedule (S - 1 even: a slot pair never straddles two rows).
+// Step t takes pair q(t) = a (S-1)/2 + cp with cp = t / S, a = t % S: the pairs
+// of one column pair cp = c/2 for every row a, then the next cp.  Receiver
+// b = c + (c >= a) of a slot (a, c) stays within {c, c+1, c+2}, so a column is
+// complete a few steps after it starts and its majority is taken right then:
+// about three columns' counters are live at a time instead of all S (row order
+// feeds every column from the first row to the last).  Counts do not depend on
+// the input order, so the results are identical.
+struct LeafSched {
+    static constexpr int slot_recv(int S, int e) {
+        const int a = e / (S - 1), c = e % (S - 1);
+        return c + (c >= a ? 1 : 0);
+    }
+    static constexpr int step_pair(int S, int t) { return (t % S) * ((S - 1) / 2) + t / S; }
+    // inputs column b holds before slot h of step t (its diag value counts as one)
+    static constexpr int inputs_before(int S, int b, int t, int h) {
+        int k = 1;
+        for (int u = 0; u <= t; ++u)
+            for (int hh = 0; hh < 2; ++hh) {
+                if (u == t && hh >= h) return k;
+                if (slot_recv(S, 2 * step_pair(S, u) + hh) == b) ++k;
+            }
+        return k;
+    }
+    static constexpr int last_step(int S, int b) {
+        int last = -1;
+        for (int u = 0; u < S * (S - 1) / 2; ++u)
+            for (int hh = 0; hh < 2; ++hh)
+                if (slot_recv(S, 2 * step_pair(S, u) + hh) == b) last = u;
+        return last;
+    }
+};
+
+// emit(b, R_b) receives column b's majority as soon as the column is complete
+// (a caller that stores it right away keeps no result registers live).
+template <int S, typename Emit>
+__device__ __forceinline__ void leaf_block_cols(uint32_t me, uint64_t seed, uint64_t gw,
+                                                uint32_t sr, const uint64_t (&diag)[S],
+                                                const uint64_t (&Fm)[S], Emit&& emit) {
+    constexpr int NL = planes_c(S);
+    constexpr int NPAIR = S * (S - 1) / 2;
+    constexpr int PG = leaf_philox_group(NPAIR);
+    Csa<NL> cnt[S];
+    static_for<0, S>([&](auto b) { cnt[b()].template add<0>(diag[b()]); });
+    const uint32_t pair0 = sr * (uint32_t)NPAIR;
+    static_for<0, (NPAIR + PG - 1) / PG>([&](auto grp) {
+        constexpr int t0 = grp() * PG, ng = NPAIR - t0 < PG ? NPAIR - t0 : PG;
+        P4 c[ng];
+        static_for<0, ng>([&](auto g) {
+            c[g()] = P4{pair0 + (uint32_t)LeafSched::step_pair(S, t0 + g()), me, (uint32_t)gw,
+                        (uint32_t)(gw >> 32)};
+        });
+        philox10_n<ng>(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+        static_for<0, ng>([&](auto g) {
+            constexpr int t = t0 + g(), q = LeafSched::step_pair(S, t);
+            static_for<0, 2>([&](auto h) {
+                constexpr int e = 2 * q + h();
+                constexpr int a = e / (S - 1);
+                constexpr int b = LeafSched::slot_recv(S, e);
+                constexpr int K = LeafSched::inputs_before(S, b, t, h());
+                const uint64_t lw = h() == 0 ? ((uint64_t)c[g()].y << 32 | c[g()].x)
+                                             : ((uint64_t)c[g()].w << 32 | c[g()].z);
+                cnt[b].template add<K>((Fm[a] & lw) | (~Fm[a] & diag[a]));
+            });
+            // columns whose last input was this step: majority now, counters die
+            static_for<0, S>([&](auto b) {
+                if constexpr (LeafSched::last_step(S, b()) == t)
+                    emit(b, cnt[b()].template ge<S, S / 2 + 1>());
+            });
+        });
+    });
+}
+
 template <int S>
 __device__ __forceinline__ void leaf_block(uint32_t me, uint64_t seed, uint64_t gw, uint32_t sr,
                                            const uint64_t (&diag)[S], const uint64_t (&Fm)[S],
                                            uint64_t (&R)[S]) {
+#ifndef BA_LEAF_ROW_ORDER
+    if constexpr (S >= 3 && (S - 1) % 2 == 0) {
+        leaf_block_cols<S>(me, seed, gw, sr, diag, Fm,
+                           [&](auto b, uint64_t v) { R[b()] = v; });
+        return;
+    }
+#endif
     constexpr int NL = planes_c(S);
     constexpr int NPAIR = S * (S - 1) / 2;
     constexpr int PG = leaf_philox_group(NPAIR);
@@ -56,6 +136,24 @@ __device__ __forceinline__ void leaf_block(uint32_t me, uint64_t seed, uint64_t 
     });
     // S inputs per column; strict majority, inner tie -> non-attack
     static_for<0, S>([&](auto b) { R[b()] = cnt[b()].template ge<S, S / 2 + 1>(); });
+}
+
+// leaf_block with the results handed to emit(b, R_b) (std::integral_constant b):
+// right when each column completes under the column schedule, at the end
+// otherwise.
+template <int S, typename Emit>
+__device__ __forceinline__ void leaf_block_emit(uint32_t me, uint64_t seed, uint64_t gw,
+                                                uint32_t sr, const uint64_t (&diag)[S],
+                                                const uint64_t (&Fm)[S], Emit&& emit) {
+#ifndef BA_LEAF_ROW_ORDER
+    if constexpr (S >= 3 && (S - 1) % 2 == 0) {
+        leaf_block_cols<S>(me, seed, gw, sr, diag, Fm, emit);
+        return;
+    }
+#endif
+    uint64_t R[S];
+    leaf_block<S>(me, seed, gw, sr, diag, Fm, R);
+    static_for<0, S>([&](auto b) { emit(b, R[b()]); });
 }
 
 // Bit-sliced count of one matrix column in an LDS word image: the direct value

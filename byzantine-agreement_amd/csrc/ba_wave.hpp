@@ -672,25 +672,23 @@ __device__ __forceinline__ uint64_t om3_round(const uint64_t* in, uint64_t l0j1,
         const uint64_t par = (fj & lie) | (~fj & l0j1);
         // 2. leaf block (j1, a): level-2 diagonal (sender j2), then S(S-1) leaves
         const uint64_t oddmask = 0ull - (uint64_t)(x0 & 1u);
-        uint64_t diag[S], R[S];
+        uint64_t diag[S];
         static_for<0, S>([&](auto a) {
             uint64_t lie2;
             if constexpr (S % 2 == 1) lie2 = lw2[a()] ^ ((lw2[a()] ^ lw2[a() + 1]) & oddmask);
             else lie2 = lw2[a()];
             diag[a()] = (fs & lie2) | (~fs & par);
         });
-        leaf_block<S>(ME, seed, gw, sr, diag, Fm, R);
         // receiver-major: member d of block a is receiver b = d + (d >= a)
         uint64_t* r2t = r2t_w + lw * C * CP + la;
+        char* rb = (char*)r2t;
+        leaf_block_emit<S>(ME, seed, gw, sr, diag, Fm, [&](auto d, uint64_t v) {
+            if constexpr (EROW)
+                *(uint64_t*)(rb + ofs.r2t.template get<d()>() + 8 * CP * d()) = v;
+            else
+                r2t[(d() + (d() >= la ? 1u : 0u)) * CP] = v;
+        });
         r2t[la * CP] = par;
-        if constexpr (EROW) {
-            char* rb = (char*)r2t;
-            static_for<0, S>([&](auto d) {
-                *(uint64_t*)(rb + ofs.r2t.template get<d()>() + 8 * CP * d()) = R[d()];
-            });
-        } else {
-            static_for<0, S>([&](auto d) { r2t[(d() + (d() >= la ? 1u : 0u)) * CP] = R[d()]; });
-        }
     }
     __builtin_amdgcn_wave_barrier();
     uint64_t r1 = 0;
@@ -722,6 +720,7 @@ template <int N>
 struct Om3W {
     static constexpr int L = N - 1, S = N - 3, C = L - 1;
     static constexpr int W = 64 / C;               // trial words per wave task
+    static constexpr int BPC = 2;                  // launch cap: blocks per CU
     static constexpr int LANES = W * C;            // lanes busy in the subtree rounds
     static constexpr int NIN = N + 3;
     static constexpr int CP = C + 1;               // padded R2T row (om3_round)
@@ -1237,10 +1236,18 @@ inline hipError_t launch_om3q(const RunArgs& a) {
 // LDS per wave: IN[W][N+3] | L0[W][L] | R3T[W][C2][C2] | R1C[W][C1][P1] |
 // RC[W][L][P] ; A/U roots reuse R3T when it fits.
 // ---------------------------------------------------------------------------
+// k_om4w's occupancy target: 3 blocks of 4 waves per CU (3 waves per SIMD,
+// <= 168 VGPRs; the launch cap below follows it).  Round 3: the column-ordered
+// leaf schedule and staged inputs brought the kernel from 224 to 186 VGPRs, and
+// the 3-wave bound costs a few spills outside the round loop (per first hop).
+#ifndef BA_OM4W_BLOCKS_PER_CU
+#define BA_OM4W_BLOCKS_PER_CU 3
+#endif
 template <int N>
 struct Om4W {
     static constexpr int L = N - 1, S = N - 4, C1 = L - 1, C2 = L - 2;
     static constexpr int W = 64 / C2;
+    static constexpr int BPC = BA_OM4W_BLOCKS_PER_CU;  // launch cap: blocks per CU
     static constexpr int LANES = W * C2;
     static constexpr int P = planes_c(L), P1 = planes_c(C1);
     static constexpr int NIN = N + 3;
@@ -1253,8 +1260,8 @@ struct Om4W {
     static constexpr int words = ((au_in_r3 ? end0 : end0 + W * 2 * L) + 1) & ~1;
 };
 
-template <int N>
-__global__ __launch_bounds__(kWaveThreads, 2) void k_om4w(
+template <int N, bool STAGED = false>
+__global__ __launch_bounds__(kWaveThreads, BA_OM4W_BLOCKS_PER_CU) void k_om4w(
     uint64_t seed, GenSpec gs, uint64_t first_trial, uint64_t batch,
     const uint32_t* __restrict__ faulty, const uint8_t* __restrict__ order,
     uint64_t* __restrict__ decisions, uint8_t* __restrict__ outcome,
@@ -1288,7 +1295,10 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om4w(
         if (sk.tasks != nullptr && lane == 0) next_raw = atomicAdd(sk.tasks, 1u);
         const uint64_t w0 = task * W;
         const uint64_t gw0 = (first_trial >> 6) + w0;
-        wave_inputs<N, W, 0>(img + G::oIN, lane, w0, seed, gs, first_trial, batch, faulty, order);
+        if constexpr (STAGED)
+            stage_words<N, W>(img + G::oIN, lane, w0, batch, faulty, order);
+        else
+            wave_inputs<N, W, 0>(img + G::oIN, lane, w0, seed, gs, first_trial, batch, faulty, order);
         __builtin_amdgcn_wave_barrier();
         wave_level0<N, W, P>(img + G::oIN, img + G::oL0, img + G::oRC, lane, seed, gw0);
         __builtin_amdgcn_wave_barrier();
@@ -1337,7 +1347,9 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om4w(
                     });
                     pc[NPD] = P4{x2 >> 1, 2u, (uint32_t)gw, (uint32_t)(gw >> 32)};
                     pc[NPD + 1] = P4{x1 >> 1, 1u, (uint32_t)gw, (uint32_t)(gw >> 32)};
-                    philox10_n<NPD + 2>(pc, (uint32_t)seed, (uint32_t)(seed >> 32));
+                    // at most 4 calls in flight (philox10_n's one-statement rounds;
+                    // 7 interleaved calls held ~70 VGPRs at once)
+                    philox_groups<NPD + 2>(pc, (uint32_t)seed, (uint32_t)(seed >> 32));
                     uint64_t lw3[2 * NPD];
                     static_for<0, NPD>([&](auto qd) {
                         lw3[2 * qd()] = (uint64_t)pc[qd()].y << 32 | pc[qd()].x;
@@ -1355,7 +1367,7 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om4w(
                     const uint64_t fs = erow[la];  // level-3 sender: j3
                     const uint64_t oddmask = 0ull - (uint64_t)(x3 & 1u);
                     const char* eb = (const char*)erow;
-                    uint64_t diag[S], Fm[S], R[S];
+                    uint64_t diag[S], Fm[S];
                     static_for<0, S>([&](auto d) {
                         uint64_t lie3;
                         if constexpr (S % 2 == 1) lie3 = lw3[d()] ^ ((lw3[d()] ^ lw3[d() + 1]) & oddmask);
@@ -1363,13 +1375,12 @@ __global__ __launch_bounds__(kWaveThreads, 2) void k_om4w(
                         diag[d()] = (fs & lie3) | (~fs & par);
                         Fm[d()] = *(const uint64_t*)(eb + memr.template get<d()>());
                     });
-                    leaf_block<S>(ME, seed, gw, x2, diag, Fm, R);
                     uint64_t* r3t = img + G::oR3 + lw * C2 * C2 + la;
-                    r3t[la * C2] = par;
                     char* rb = (char*)r3t;
-                    static_for<0, S>([&](auto d) {
-                        *(uint64_t*)(rb + r3r.template get<d()>() + 8 * C2 * d()) = R[d()];
+                    leaf_block_emit<S>(ME, seed, gw, x2, diag, Fm, [&](auto d, uint64_t v) {
+                        *(uint64_t*)(rb + r3r.template get<d()>() + 8 * C2 * d()) = v;
                     });
+                    r3t[la * C2] = par;
                 }
                 __builtin_amdgcn_wave_barrier();
                 if (act) {
@@ -1424,7 +1435,7 @@ inline hipError_t launch_wave(const RunArgs& a, K kernel, const char* name, K st
     constexpr uint32_t wpb = kWaveThreads / 64;
     const uint64_t words = (a.batch + 63) / 64, tasks = (words + G::W - 1) / G::W;
     uint64_t blocks = (tasks + wpb - 1) / wpb;
-    uint64_t cap = 2ull * a.cu_count;
+    uint64_t cap = (uint64_t)G::BPC * a.cu_count;
     if (const char* e = getenv("BA_WAVE_MAX_BLOCKS")) {  // tests: force the persistent task loop
         const uint64_t c = strtoull(e, nullptr, 0);
         if (c >= 1 && c < cap) cap = c;

@@ -78,10 +78,44 @@ def main():
         n, m, T = 13, 4, a.trials3
         D.run_trials_dp(comm, n, m, 1 << 16, f=4)  # warm-up: geometry, scratch
         cnt, dt = timed(lambda: D.run_trials_dp(comm, n, m, T, f=4), world, dev)
-        out.append({"config": 3, "workload": f"OM({m}) n={n}, {T} trials, f~U{{0..4}}, "
-                    f"trial-DP over {world} GPU(s), counters all-reduced",
-                    "trials_per_s": T / dt, "seconds": dt, "n_gpus": world,
-                    "counters": counters(cnt)})
+        rec = {"config": 3, "workload": f"OM({m}) n={n}, {T} trials, f~U{{0..4}}, "
+               f"trial-DP over {world} GPU(s), counters all-reduced",
+               "trials_per_s": T / dt, "seconds": dt, "n_gpus": world,
+               "counters": counters(cnt)}
+        if world == 1:
+            # the same trials with their inputs staged in HBM before timing (as
+            # bench.py): one ba_run_trials_device call of all T trials on a stream;
+            # its counters must equal the in-kernel-draw run's
+            p = L.make_params(n, m, 0xBA5EED, L.LIE_PHILOX, L.FAULTY_RANDOM, 4, L.ORDER_RANDOM,
+                              L.ATTACK, L.ENGINE_AUTO, 0)
+            pg = L.make_params(n, m, 0xBA5EED, L.LIE_PHILOX, L.FAULTY_GIVEN, 4, L.ORDER_GIVEN,
+                               L.ATTACK, L.ENGINE_AUTO, 0)
+            st = torch.cuda.Stream(dev)
+            fb = torch.empty(T, dtype=torch.int32, device=dev)
+            ob = torch.empty(T, dtype=torch.uint8, device=dev)
+            sd = torch.empty(T, dtype=torch.int64, device=dev)
+            so = torch.empty(T, dtype=torch.uint8, device=dev)
+            sc = torch.zeros(16, dtype=torch.int64, device=dev)
+            eng.gen_inputs_device(p, T, d_faulty=fb.data_ptr(), d_order=ob.data_ptr(),
+                                  stream=st.cuda_stream)
+
+            def call3():
+                eng.run_device(pg, T, d_faulty=fb.data_ptr(), d_order=ob.data_ptr(),
+                               d_decisions=sd.data_ptr(), d_outcome=so.data_ptr(),
+                               d_counters=sc.data_ptr(), stream=st.cuda_stream)
+            call3()  # warm-up
+            torch.cuda.synchronize(dev)
+            sc.zero_()
+            torch.cuda.synchronize(dev)
+            _, sdt = timed(call3, world, dev)
+            if counters(sc) != counters(cnt):
+                raise SystemExit("config 3: staged-input counters differ from the in-kernel run")
+            rec["trials_per_s_staged"] = T / sdt
+            rec["seconds_staged"] = sdt
+            rec["staged_note"] = ("inputs staged in HBM before timing (as bench.py), one "
+                                  "ba_run_trials_device call; counters equal the in-kernel run")
+            del fb, ob, sd, so
+        out.append(rec)
 
     if 4 in which:
         n, m, T = 10, 3, a.trials4
