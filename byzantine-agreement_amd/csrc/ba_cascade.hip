@@ -31,6 +31,11 @@
 //
 // Bit-identical to the LEVELS pipeline: same lie keying (level, global slot
 // pair, global word), same majorities and epilogue.
+//
+// The carry-save thresholds here use the resolve-then-compare form: the level-bit
+// form (Csa::ge_from, the WAVE kernels' default) took k_cascade<16,5> from 126
+// to 142 VGPRs (4 -> 3 waves per SIMD) for ~1% fewer instructions.
+#define BA_CSA_GE_RESOLVE 1
 #include "ba_wave.hpp"
 
 namespace ba {

@@ -396,11 +396,51 @@ struct Csa {
             }
         }
     }
+    // Largest count the events from level L up can still represent (N events
+    // pushed into level L), in units of 2^L.
+    static constexpr int max_units(int L, int N) {
+        if (L >= NL || N <= 0) return 0;
+        const int nb = (N >= 1 ? 1 : 0) + (N >= 2 && N % 2 == 0 ? 1 : 0);
+        return nb + 2 * max_units(L + 1, N >= 1 ? (N - 1) / 2 : 0);
+    }
+    // Lanes whose count from level L up (units of 2^L) is >= TH, straight from
+    // the level bits (acc, pend) without resolving the binary sum: one level's
+    // one or two bits decide between two neighbouring thresholds of the levels
+    // above, G(t) and G(t + 1) with G(t) >= G(t + 1), so each step is
+    // G(t+1) | (c & G(t)): about one 3-input op per level (majority of 9 from
+    // the carry-save state: 3 ops per 32-bit half, where the ripple resolve and
+    // the compare chain took ~8).
+    template <int L, int N, int TH>
+    __host__ __device__ __forceinline__ T ge_from() const {
+        if constexpr (TH <= 0) return (T)~(T)0;
+        else if constexpr (TH > max_units(L, N)) return (T)0;
+        else {
+            constexpr bool hasA = N >= 1, hasP = N >= 2 && N % 2 == 0;
+            constexpr int up = N >= 1 ? (N - 1) / 2 : 0;
+            if constexpr (!hasA && !hasP) {
+                return ge_from<L + 1, up, (TH + 1) / 2>();
+            } else if constexpr (hasA != hasP) {
+                const T b = hasA ? acc[L] : pend[L];
+                if constexpr (TH % 2 == 0) return ge_from<L + 1, up, TH / 2>();
+                else return ge_from<L + 1, up, (TH + 1) / 2>() | (b & ge_from<L + 1, up, (TH - 1) / 2>());
+            } else if constexpr (TH % 2 == 0) {
+                // two bits: their sum is 2 iff both
+                return ge_from<L + 1, up, TH / 2>() | (acc[L] & pend[L] & ge_from<L + 1, up, TH / 2 - 1>());
+            } else {
+                // sum >= 1 iff either
+                return ge_from<L + 1, up, (TH + 1) / 2>() |
+                       ((acc[L] | pend[L]) & ge_from<L + 1, up, (TH - 1) / 2>());
+            }
+        }
+    }
     // lanes whose count (after K inputs) is >= TH
     template <int K, int TH>
     __host__ __device__ __forceinline__ T ge() const {
         if constexpr (TH <= 0) return (T)~(T)0;
         else if constexpr (TH > K) return (T)0;
+#ifndef BA_CSA_GE_RESOLVE
+        else if constexpr (true) return ge_from<0, K, TH>();
+#endif
         else {
             T r[NL];
             resolve<0, K, false>(r, 0);

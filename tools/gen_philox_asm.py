@@ -162,8 +162,10 @@ def main():
            '                                               uint32_t (&z)[G], uint32_t (&w)[G],',
            '                                               const uint32_t (&k0)[8], const uint32_t (&k1)[8]);',
            '']
+    out.append('#ifdef __HIP_DEVICE_COMPILE__  // device code only (host passes never call it)')
     for G in (2, 3, 4):
         out.append(gen(G))
+    out.append('#endif')
     out.append('}  // namespace ba')
     print("\n".join(out))
 
