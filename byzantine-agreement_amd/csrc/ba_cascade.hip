@@ -36,6 +36,9 @@
 // form (Csa::ge_from, the WAVE kernels' default) took k_cascade<16,5> from 126
 // to 142 VGPRs (4 -> 3 waves per SIMD) for ~1% fewer instructions.
 #define BA_CSA_GE_RESOLVE 1
+#ifdef BA_CASCADE_SKEYS  // A/B: Philox round keys as SGPR operands in this TU
+#define BA_PHILOX_SKEYS 1
+#endif
 #include "ba_wave.hpp"
 
 namespace ba {

@@ -173,11 +173,91 @@ __device__ __forceinline__ uint32_t as_vgpr(uint32_t k) {
     return r;
 }
 #endif
+// The key schedule of one seed in VGPRs (kv0[i], kv1[i] = round i's keys): a
+// VALU op with an SGPR operand issues slower than one with VGPR operands only
+// (tools/valu_cost operands: v_bitop3 xor3 4.5 vs 2.7 cycles per wave64
+// instruction at 8 waves/SIMD), and every Philox xor3 takes one key.  The empty
+// asm keeps the (uniform) values in VGPRs.
+struct KeysV {
+    uint32_t k0[10], k1[10];
+    __device__ __forceinline__ explicit KeysV(uint64_t seed)
+        : KeysV((uint32_t)seed, (uint32_t)(seed >> 32)) {}
+    // the asm is not volatile: a pure function of the seed, so the compiler can
+    // hoist it out of the loops and share it between call sites
+    __device__ __forceinline__ KeysV(uint32_t a, uint32_t b) {
+#pragma unroll
+        for (int i = 0; i < 10; ++i) {
+            k0[i] = a + (uint32_t)i * 0x9E3779B9u;
+            k1[i] = b + (uint32_t)i * 0xBB67AE85u;
+            asm("" : "+v"(k0[i]), "+v"(k1[i]));
+        }
+    }
+};
+
+// philox10_n with the round keys as VGPR operands (KeysV); same results.
+template <int G>
+__device__ __forceinline__ void philox10_n_vk(P4 (&c)[G], const KeysV& kv) {
+    static_for_h<0, 2>([&](auto i) {
+        uint64_t p0[G], p1[G];
+        philox_mul2_n<i(), G>(c, p0, p1);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            P4 n;
+            n.x = xor3_32((uint32_t)(p1[g] >> 32), c[g].y, kv.k0[i()]);
+            n.y = (uint32_t)p1[g];
+            n.z = xor3_32((uint32_t)(p0[g] >> 32), c[g].w, kv.k1[i()]);
+            n.w = (uint32_t)p0[g];
+            c[g] = n;
+        }
+    });
+    if constexpr (G >= 2 && G <= 4) {
+        uint32_t rk0[8], rk1[8], x[G], y[G], z[G], w[G];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            rk0[i] = kv.k0[i + 2];
+            rk1[i] = kv.k1[i + 2];
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            x[g] = c[g].x;
+            y[g] = c[g].y;
+            z[g] = c[g].z;
+            w[g] = c[g].w;
+        }
+        philox_r29_asm_vk<G>(x, y, z, w, rk0, rk1);
+#pragma unroll
+        for (int g = 0; g < G; ++g) c[g] = P4{x[g], y[g], z[g], w[g]};
+    } else {
+        static_for_h<2, 10>([&](auto i) {
+            uint64_t p0[G], p1[G];
+            philox_mul2_n<i(), G>(c, p0, p1);
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                P4 n;
+                n.x = xor3_32((uint32_t)(p1[g] >> 32), c[g].y, kv.k0[i()]);
+                n.y = (uint32_t)p1[g];
+                n.z = xor3_32((uint32_t)(p0[g] >> 32), c[g].w, kv.k1[i()]);
+                n.w = (uint32_t)p0[g];
+                c[g] = n;
+            }
+        });
+    }
+}
+
 template <int G>
 __host__ __device__ __forceinline__ void philox10_n(P4 (&c)[G], uint32_t k0, uint32_t k1) {
 #if defined(__HIP_DEVICE_COMPILE__) && defined(BA_PHILOX_VKEYS)
     k0 = as_vgpr(k0);
     k1 = as_vgpr(k1);
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(BA_PHILOX_C) && !defined(BA_PHILOX_ROUND_ASM) && \
+    !defined(BA_PHILOX_SKEYS)
+    // round keys as VGPR operands (KeysV, hoisted by the compiler): Philox calls
+    // 8.4e11 -> 9.6e11 per second at 2 waves/SIMD (tools/philox_bench)
+    if constexpr (G >= 2 && G <= 4) {
+        philox10_n_vk<G>(c, KeysV(k0, k1));
+        return;
+    }
 #endif
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(BA_PHILOX_C) && !defined(BA_PHILOX_ROUND_ASM)
     // rounds 0-1 in C (the compiler shares and strength-reduces the products a

@@ -778,8 +778,17 @@ __device__ __forceinline__ void roots_r1t(const uint64_t* r1t0, uint64_t* au, ui
 // DIAG: lab-only ablation switches (tools/om3_lab.hip); the product uses 0.
 // STAGED: both inputs given (ba_gen_inputs_device buffers): the task's inputs
 // are loads and ballots only, the draw code is not compiled in.
+// Occupancy target: 3 blocks of 4 waves per CU (<= 168 VGPRs, 3 waves/SIMD: a
+// second step in flight fills the third slot) for n <= 10; the larger trees
+// (172-215 VGPRs) stay at 2 rather than spill.  Round 3, one box's A/B
+// (profiles/r03h_ab_vgpr_keys.log): the n=10 kernel at 168 VGPRs (2 spills)
+// ran 50.3 us vs 50.4 us at 170, and the two-step bench 2.41-2.44e10 vs
+// 2.26-2.31e10.
+#ifndef BA_OM3W_MIN_BLOCKS
+#define BA_OM3W_MIN_BLOCKS(n) ((n) <= 10 ? 3 : 2)
+#endif
 template <int N, int DIAG = 0, bool STAGED = false>
-__global__ __launch_bounds__(kWaveThreads, 2) void k_om3w(
+__global__ __launch_bounds__(kWaveThreads, BA_OM3W_MIN_BLOCKS(N)) void k_om3w(
     uint64_t seed, GenSpec gs, uint64_t first_trial, uint64_t batch,
     const uint32_t* __restrict__ faulty, const uint8_t* __restrict__ order,
     uint64_t* __restrict__ decisions, uint8_t* __restrict__ outcome,

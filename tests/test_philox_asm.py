@@ -34,9 +34,9 @@ def philox_rounds(c, k0, k1, r0, r1):
     return [x, y, z, w]
 
 
-def parse(G):
+def parse(G, name="philox_r29_asm"):
     src = open(HDR).read()
-    m = re.search(r"philox_r29_asm<%d>\(.*?asm volatile\((.*?)\);\n}" % G, src, re.S)
+    m = re.search(r"%s<%d>\(.*?asm volatile\((.*?)\);\n}" % (name, G), src, re.S)
     assert m, f"no G={G} specialisation"
     body = m.group(1)
     parts = body.split("\n        : ")
@@ -100,9 +100,10 @@ def run_asm(lines, outs, ins, env):
     return out
 
 
+@pytest.mark.parametrize("name", ["philox_r29_asm", "philox_r29_asm_vk"])
 @pytest.mark.parametrize("G", [2, 3, 4])
-def test_generated_rounds_match_philox(G):
-    lines, outs, ins = parse(G)
+def test_generated_rounds_match_philox(G, name):
+    lines, outs, ins = parse(G, name)
     rng = random.Random(1234 + G)
     for _ in range(50):
         k0, k1 = rng.getrandbits(32), rng.getrandbits(32)

@@ -32,7 +32,7 @@ import os
 MODE = os.environ.get("PHILOX_ASM_MODE", "rot")  # "rot": 3 pairs per call; "pairs4": 4
 
 
-def gen(G: int) -> str:
+def gen(G: int, kc: str = "s") -> str:
     # operand numbering: outputs first (x[g], z[g] in/out; w[g], y[g] fixed), then
     # inputs (y_in[g], w_in[g], keys k0[0..7], k1[0..7], M0, M1), cc last output
     ops_out, ops_in = [], []
@@ -56,9 +56,9 @@ def gen(G: int) -> str:
     for g in range(G):
         ops_in.append(f'"v"(wi[{g}])')
     for i in range(8):
-        ops_in.append(f'"s"(k0[{i}])')
+        ops_in.append(f'"{kc}"(k0[{i}])')
     for i in range(8):
-        ops_in.append(f'"s"(k1[{i}])')
+        ops_in.append(f'"{kc}"(k1[{i}])')
     ops_in.append('"s"(0xD2511F53u)')
     ops_in.append('"s"(0xCD9E8D57u)')
     X = lambda g: g
@@ -132,8 +132,9 @@ def gen(G: int) -> str:
     for g in range(G):
         ops_out = [o.replace(f"vW{g}}}", f"v{outs_w[g]}}}").replace(f"vY{g}}}", f"v{outs_y[g]}}}") for o in ops_out]
     body = "\n".join(f'        "{l}\\n\\t"' for l in lines[:-1]) + f'\n        "{lines[-1]}"'
+    fname = "philox_r29_asm" if kc == "s" else "philox_r29_asm_vk"
     return f"""template <>
-__device__ __forceinline__ void philox_r29_asm<{G}>(uint32_t (&x)[{G}], uint32_t (&y)[{G}],
+__device__ __forceinline__ void {fname}<{G}>(uint32_t (&x)[{G}], uint32_t (&y)[{G}],
                                                  uint32_t (&z)[{G}], uint32_t (&w)[{G}],
                                                  const uint32_t (&k0)[8], const uint32_t (&k1)[8]) {{
     uint32_t yi[{G}], wi[{G}];
@@ -161,10 +162,18 @@ def main():
            '__device__ __forceinline__ void philox_r29_asm(uint32_t (&x)[G], uint32_t (&y)[G],',
            '                                               uint32_t (&z)[G], uint32_t (&w)[G],',
            '                                               const uint32_t (&k0)[8], const uint32_t (&k1)[8]);',
+           '// the same with the round keys as VGPR operands (VALU ops with an SGPR operand',
+           '// issue slower: tools/valu_cost operands)',
+           'template <int G>',
+           '__device__ __forceinline__ void philox_r29_asm_vk(uint32_t (&x)[G], uint32_t (&y)[G],',
+           '                                                  uint32_t (&z)[G], uint32_t (&w)[G],',
+           '                                                  const uint32_t (&k0)[8], const uint32_t (&k1)[8]);',
            '']
     out.append('#ifdef __HIP_DEVICE_COMPILE__  // device code only (host passes never call it)')
     for G in (2, 3, 4):
         out.append(gen(G))
+    for G in (2, 3, 4):
+        out.append(gen(G, "v"))
     out.append('#endif')
     out.append('}  // namespace ba')
     print("\n".join(out))

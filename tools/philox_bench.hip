@@ -4,6 +4,7 @@
 //   xor3    : v_mad_u64_u32 + v_bitop3 xor3 (2 x 3-input xors per round)
 //   mulhilo : v_mul_hi_u32 + v_mul_lo_u32 + xor3
 //   kernel_shape : ba::philox10_n as the OM kernels run it (pinned mads)
+//   kernel_shape_vgpr_keys : ba::philox10_n_vk (round keys as VGPR operands)
 // Each thread runs K independent counter-mode calls in CH interleaved chains
 // and xors the outputs (so nothing is dead code).  Measured at 1, 2, 4 and 8
 // resident waves per SIMD, after a warm-up, with the in-kernel clock.
@@ -70,12 +71,15 @@ __global__ __launch_bounds__(256) void k_philox(uint64_t seed, uint32_t K, uint3
     uint32_t acc[CH];
 #pragma unroll
     for (int c = 0; c < CH; ++c) acc[c] = 0;
+    const ba::KeysV kv(seed);
     for (uint32_t i = 0; i < K; i += CH) {
         P4 o[CH];
 #pragma unroll
         for (int c = 0; c < CH; ++c) o[c] = P4{i + c, 3u, t, 0u};
         if constexpr (V == 3) {
             ba::philox10_n<CH>(o, (uint32_t)seed, (uint32_t)(seed >> 32));
+        } else if constexpr (V == 7) {
+            ba::philox10_n_vk<CH>(o, kv);
         } else {
 #pragma unroll
             for (int c = 0; c < CH; ++c) o[c] = philox_any<V>(o[c], (uint32_t)seed, (uint32_t)(seed >> 32));
@@ -140,6 +144,9 @@ int main() {
     for (uint32_t W : {1u, 2u, 4u, 8u}) {
         run<1, 4>("xor3", W, d, st);
         run<3, 3>("kernel_shape", W, d, st);
+        run<7, 3>("kernel_shape_vgpr_keys", W, d, st);
+        run<3, 4>("kernel_shape_g4", W, d, st);
+        run<7, 4>("kernel_shape_g4_vgpr_keys", W, d, st);
     }
     (void)hipFree(d);
     (void)hipFree(st);

@@ -11,11 +11,14 @@
 #include <cstdio>
 #include <vector>
 
-enum Op { XOR3, ADD, MAD64, MULLO, MULHI, BFI, MAD24, LSHL_OR, XOR3_V, MAD64_V, ADD_S, ADD3_V };
+enum Op { XOR3, ADD, MAD64, MULLO, MULHI, BFI, MAD24, LSHL_OR, XOR3_V, MAD64_V, ADD_S, ADD3_V,
+          ADD_LIT, XOR_E32, XOR_E64, ADD_E64 };
 static const char* kNames[] = {"v_bitop3_b32(xor3)", "v_add_u32", "v_mad_u64_u32", "v_mul_lo_u32",
                                "v_mul_hi_u32", "v_bfi_b32", "v_mad_u32_u24", "v_lshl_or_b32",
                                "v_bitop3_b32(xor3, all VGPR)", "v_mad_u64_u32(VGPR multiplier)",
-                               "v_add_u32(SGPR src0)", "v_add3_u32(all VGPR)"};
+                               "v_add_u32(SGPR src0)", "v_add3_u32(all VGPR)",
+                               "v_add_u32(literal src0, 8-byte VOP2)", "v_xor_b32_e32",
+                               "v_xor_b32_e64 (VOP3 encoding)", "v_add_u32_e64 (VOP3 encoding)"};
 constexpr int CH = 16;
 
 // One asm statement issues the instruction once on each of 8 independent
@@ -80,6 +83,26 @@ __device__ __forceinline__ void op8(uint32_t (&a)[8], uint64_t (&r)[8], uint32_t
                      : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
                        "+v"(a[6]), "+v"(a[7])
                      : "v"(x), "v"(m));
+    } else if constexpr (OP == ADD_LIT) {
+        asm volatile("v_add_u32 %0, 0x12345, %0\n\tv_add_u32 %1, 0x12345, %1\n\tv_add_u32 %2, 0x12345, %2\n\tv_add_u32 %3, 0x12345, %3\n\tv_add_u32 %4, 0x12345, %4\n\tv_add_u32 %5, 0x12345, %5\n\tv_add_u32 %6, 0x12345, %6\n\tv_add_u32 %7, 0x12345, %7"
+                     : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
+                       "+v"(a[6]), "+v"(a[7])
+                     : "v"(x), "s"(m));
+    } else if constexpr (OP == XOR_E32) {
+        asm volatile("v_xor_b32_e32 %0, %8, %0\n\tv_xor_b32_e32 %1, %8, %1\n\tv_xor_b32_e32 %2, %8, %2\n\tv_xor_b32_e32 %3, %8, %3\n\tv_xor_b32_e32 %4, %8, %4\n\tv_xor_b32_e32 %5, %8, %5\n\tv_xor_b32_e32 %6, %8, %6\n\tv_xor_b32_e32 %7, %8, %7"
+                     : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
+                       "+v"(a[6]), "+v"(a[7])
+                     : "v"(x), "s"(m));
+    } else if constexpr (OP == XOR_E64) {
+        asm volatile("v_xor_b32_e64 %0, %8, %0\n\tv_xor_b32_e64 %1, %8, %1\n\tv_xor_b32_e64 %2, %8, %2\n\tv_xor_b32_e64 %3, %8, %3\n\tv_xor_b32_e64 %4, %8, %4\n\tv_xor_b32_e64 %5, %8, %5\n\tv_xor_b32_e64 %6, %8, %6\n\tv_xor_b32_e64 %7, %8, %7"
+                     : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
+                       "+v"(a[6]), "+v"(a[7])
+                     : "v"(x), "s"(m));
+    } else if constexpr (OP == ADD_E64) {
+        asm volatile("v_add_u32_e64 %0, %8, %0\n\tv_add_u32_e64 %1, %8, %1\n\tv_add_u32_e64 %2, %8, %2\n\tv_add_u32_e64 %3, %8, %3\n\tv_add_u32_e64 %4, %8, %4\n\tv_add_u32_e64 %5, %8, %5\n\tv_add_u32_e64 %6, %8, %6\n\tv_add_u32_e64 %7, %8, %7"
+                     : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
+                       "+v"(a[6]), "+v"(a[7])
+                     : "v"(x), "s"(m));
     } else if constexpr (OP == LSHL_OR) {
         asm volatile("v_lshl_or_b32 %0, %0, 3, %8\n\tv_lshl_or_b32 %1, %1, 3, %8\n\tv_lshl_or_b32 %2, %2, 3, %8\n\tv_lshl_or_b32 %3, %3, 3, %8\n\tv_lshl_or_b32 %4, %4, 3, %8\n\tv_lshl_or_b32 %5, %5, 3, %8\n\tv_lshl_or_b32 %6, %6, 3, %8\n\tv_lshl_or_b32 %7, %7, 3, %8"
                      : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
@@ -167,6 +190,10 @@ int main(int argc, char** argv) {
             run<ADD>(W, d, st);
             run<ADD_S>(W, d, st);
             run<ADD3_V>(W, d, st);
+            run<ADD_LIT>(W, d, st);
+            run<XOR_E32>(W, d, st);
+            run<XOR_E64>(W, d, st);
+            run<ADD_E64>(W, d, st);
             continue;
         }
         run<XOR3>(W, d, st);
