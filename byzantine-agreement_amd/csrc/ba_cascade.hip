@@ -123,32 +123,6 @@ __device__ __forceinline__ uint64_t chain_value(const CascArgs& a, const uint64_
     return v;
 }
 
-__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-__device__ __forceinline__ void store_sc1(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v,
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ uint64_t load_sc1(const uint64_t* p) {
-    return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// One arrival at counter c (lane 0 adds; every lane gets the answer): true on
-// the arrival that completes `expect`, which also resets the counter.
-__device__ __forceinline__ bool arrive_last(uint32_t* c, uint32_t expect, uint32_t lane) {
-    uint32_t old = 0;
-    if (lane == 0)
-        old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
-    const bool last = old + 1 == expect;
-    if (last && lane == 0) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // compiler ordering only: no load of the children may move above the add
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    return last;
-}
-
 // Lieutenant indices j[0..K] of the path of level-K slot x (lexicographic rank
 // over (K+1)-permutations of the L lieutenants): digit k is the rank of j[k]
 // among the lieutenants not in j[0..k-1], picked by one compare-increment per

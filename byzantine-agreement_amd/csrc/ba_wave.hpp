@@ -775,6 +775,37 @@ __device__ __forceinline__ void roots_r1t(const uint64_t* r1t0, uint64_t* au, ui
     }
 }
 
+// Hand-offs between waves of one launch through L2 (k_cascade, k_om3h): results
+// are stored write-through (sc1: relaxed agent-scope atomic stores), drained,
+// and announced with one atomic add; the arrival that completes a counter reads
+// the others' results with sc1 loads only, after its add returned.  No wave ever
+// waits for another.
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ void store_sc1(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint64_t load_sc1(const uint64_t* p) {
+    return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One arrival at counter c (lane 0 adds; every lane gets the answer): true on
+// the arrival that completes `expect`, which also resets the counter.
+__device__ __forceinline__ bool arrive_last(uint32_t* c, uint32_t expect, uint32_t lane) {
+    uint32_t old = 0;
+    if (lane == 0)
+        old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
+    const bool last = old + 1 == expect;
+    if (last && lane == 0) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // compiler ordering only: no load of the children may move above the add
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return last;
+}
+
 // DIAG: lab-only ablation switches (tools/om3_lab.hip); the product uses 0.
 // STAGED: both inputs given (ba_gen_inputs_device buffers): the task's inputs
 // are loads and ballots only, the draw code is not compiled in.
@@ -870,6 +901,95 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM3W_MIN_BLOCKS(N)) void k_om3w(
         g_fused_stamps[blockIdx.x * wpb + wv][7] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// k_om3h: k_om3w with each task split into two halves of its first-hop rounds
+// (staged inputs; BA_WAVE_SPLIT=1).  A unit is (task, half): half 0 runs rounds
+// j1 in [0, H0), half 1 rounds [H0, L), H0 = ceil(L/2).  Both halves stage the
+// task's inputs and level 0 (5 of ~230 Philox calls per word); each publishes
+// its R1 entries R1T[w][col][j1] (its j1 range) to the task's exchange block in
+// L2 and arrives at the task's counter; the second arrival merges the other
+// half's entries into its LDS image and runs the roots, the epilogue and the
+// counts.  No wave waits for another (the k_cascade hand-off), and units come
+// from the ctx's dynamic counter: 2 units per task halve the granule a wave
+// takes, so a one-step launch's tail (the SIMD's younger wave running alone
+// after its older partner finished) is about half as long.
+// xch: [tasks][W][L][L] words; xcnt: [tasks] counters, zero between launches
+// (the last arriver resets its counter).
+// ---------------------------------------------------------------------------
+template <int N>
+__global__ __launch_bounds__(kWaveThreads, BA_OM3W_MIN_BLOCKS(N)) void k_om3h(
+    uint64_t seed, GenSpec gs, uint64_t first_trial, uint64_t batch,
+    const uint32_t* __restrict__ faulty, const uint8_t* __restrict__ order,
+    uint64_t* __restrict__ decisions, uint8_t* __restrict__ outcome,
+    uint64_t* __restrict__ counters, Sink sk, uint64_t* __restrict__ xch,
+    uint32_t* __restrict__ xcnt) {
+    using G = Om3W<N>;
+    constexpr int L = G::L, C = G::C, W = G::W, NIN = G::NIN, H0 = (L + 1) / 2;
+    constexpr uint32_t ME = 3;
+    (void)gs;
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    uint64_t* img = lds + (uint64_t)wv * G::words;
+    const uint64_t total_words = (batch + 63) / 64;
+    const uint64_t ntasks = (total_words + W - 1) / W, nunits = 2 * ntasks;
+    const uint32_t lw_ = lane / C, la = lane - lw_ * C;
+    const bool act = lane < (uint32_t)G::LANES;
+    const uint32_t lw = act ? lw_ : 0;
+    const Om3LaneOffsets<N> lofs(la);
+    uint64_t folded = 0;
+    const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
+    for (uint64_t u = (uint64_t)blockIdx.x * wpb + wv; u < nunits;) {
+        uint32_t next_raw = 0;
+        if (sk.tasks != nullptr && lane == 0) next_raw = atomicAdd(sk.tasks, 1u);
+        const uint64_t task = u >> 1;
+        const uint32_t half = (uint32_t)(u & 1u);
+        const uint32_t jb = half ? (uint32_t)H0 : 0u, je = half ? (uint32_t)L : (uint32_t)H0;
+        const uint64_t w0 = task * W;
+        const uint64_t gw0 = (first_trial >> 6) + w0;
+        stage_words<N, W>(img + G::oIN, lane, w0, batch, faulty, order);
+        __builtin_amdgcn_wave_barrier();
+        level0_r1t<N, W>(img + G::oIN, img + G::oL0, img + G::oR1, lane, seed, gw0);
+        const uint64_t* in = img + G::oIN + lw * NIN;
+        uint64_t* erow = img + G::oE + lw * (C + 1);
+        // E row of round jb: the lieutenants other than jb in rank order
+        if (act) erow[la] = in[la + (la >= jb ? 1u : 0u) + 1];
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t gw = gw0 + lw;
+        for (uint32_t j1 = jb; j1 < je; ++j1) {
+            const uint64_t r1 = om3_round<N, true>(in, act ? img[G::oL0 + lw * L + j1] : 0ull,
+                                                   img + G::oR2, lw, la, act, j1, seed, gw,
+                                                   erow, &lofs);
+            if (act) img[G::oR1 + (lw * L + la + (la >= j1 ? 1u : 0u)) * L + j1] = r1;
+        }
+        __builtin_amdgcn_wave_barrier();
+        // publish this half's entries R1T[w][col][j1], j1 in [jb, je), col != j1
+        uint64_t* xt = xch + task * (uint64_t)(W * L * L);
+        const uint32_t nj = je - jb;
+        for (uint32_t it = lane; it < (uint32_t)(W * L) * nj; it += 64) {
+            const uint32_t row = it / nj, j1 = jb + (it - row * nj);  // row = w * L + col
+            if (row % L != j1) store_sc1(xt + row * L + j1, img[G::oR1 + row * L + j1]);
+        }
+        drain_stores();
+        if (arrive_last(xcnt + task, 2u, lane)) {
+            const uint32_t ob = half ? 0u : (uint32_t)H0, on = half ? (uint32_t)H0 : (uint32_t)(L - H0);
+            for (uint32_t it = lane; it < (uint32_t)(W * L) * on; it += 64) {
+                const uint32_t row = it / on, j1 = ob + (it - row * on);
+                if (row % L != j1) img[G::oR1 + row * L + j1] = load_sc1(xt + row * L + j1);
+            }
+            __builtin_amdgcn_wave_barrier();
+            roots_r1t<L, W>(img + G::oR1, img + G::oAU, lane);
+            __builtin_amdgcn_wave_barrier();
+            TrialCounts tc;
+            wave_epilogue<N, W, ME, 0>(img + G::oIN, img + G::oAU, lane, w0, batch, decisions,
+                                       outcome, tc);
+            wave_fold(tc, lane, folded);
+        }
+        __builtin_amdgcn_wave_barrier();
+        u = sk.tasks != nullptr ? nwaves + __builtin_amdgcn_readfirstlane(next_raw) : u + nwaves;
+    }
+    wave_flush_folded(folded, lane, wv, wpb, counters, sk, false);
 }
 
 // ---------------------------------------------------------------------------

@@ -323,6 +323,44 @@ def test_om3_wave_block_generic_vs_oracle(monkeypatch, n, m, f, fmode):
         assert {k: res.counters[k] for k in ocnt} == ocnt, tag
 
 
+@pytest.mark.parametrize("n", [5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
+def test_om3_split_halves_vs_oracle(monkeypatch, n):
+    """k_om3h (BA_WAVE_SPLIT=1: each task's first-hop rounds split over two units,
+    R1 entries exchanged through L2, the second arrival runs roots and epilogue)
+    against the oracle on staged (given) inputs: a ragged small batch and a
+    mid-size one, with the launch cap at 1 and 2 blocks (every unit through the
+    dynamic loop), and twice on one ctx (the arrival counters must be back at
+    zero).  The profile proves k_om3h ran."""
+    from ba_amd import lib as L
+    monkeypatch.setenv("BA_WAVE_SPLIT", "1")
+    C = n - 2
+    W = 64 // C
+    for B in (64 * W * 3 + 37, 64 * W * 301 + 5):
+        rng = np.random.default_rng(n * 7 + B)
+        fm = (rng.integers(0, 1 << n, B, dtype=np.uint64) & rng.integers(0, 1 << n, B, dtype=np.uint64)
+              & rng.integers(0, 1 << n, B, dtype=np.uint64)).astype(np.uint32)
+        oc = rng.choice([0, 1, 2], B).astype(np.uint8)
+        od, oo, ocnt = oracle_c.run(n, 3, B, seed=11, faulty=fm, order=oc, first_trial=64 * 5)
+        for cap in (None, "1", "2"):
+            if cap:
+                monkeypatch.setenv("BA_WAVE_MAX_BLOCKS", cap)
+            else:
+                monkeypatch.delenv("BA_WAVE_MAX_BLOCKS", raising=False)
+            e = L.Engine(0)
+            try:
+                e.profile(True)
+                for rep in range(2):
+                    res = e.run(n, 3, B, seed=11, faulty=fm, order=oc, first_trial=64 * 5,
+                                engine=L.ENGINE_FUSED)
+                    tag = f"n={n} B={B} cap={cap} rep={rep}"
+                    same(res.decisions, od, "decisions " + tag)
+                    same(res.outcome, oo, "outcome " + tag)
+                    assert {k: res.counters[k] for k in ocnt} == ocnt, tag
+                assert "k_om3h" in e.profile_read(), "k_om3h did not run"
+            finally:
+                e.close()
+
+
 @pytest.mark.parametrize("kind", ["0", "2"])
 @pytest.mark.parametrize("n,B", [(10, 64 * 8 * 700 + 5), (13, 64 * 5 * 600 + 63), (7, 64 * 16 * 300)])
 def test_om3_mid_batches_vs_oracle(monkeypatch, engine, n, B, kind):
