@@ -661,6 +661,7 @@ static int run_trials_device_impl(ba_ctx* ctx, const ba_params* p, uint64_t batc
                 }
                 a.wave_xch = (uint64_t*)ctx->scratch.p;
                 a.wave_cnt = (uint32_t*)ctx->casc.p;
+                a.wave_parts = wave_split_parts();
             }
         }
         HIP_TRY(launch_fused(a, g, ge->plan_ok, ge->fp, (const FusedPlan*)ge->fplan.p,

@@ -51,6 +51,7 @@ struct RunArgs {
     // counters (ctx scratch; nullptr = no split)
     uint64_t* wave_xch = nullptr;
     uint32_t* wave_cnt = nullptr;
+    uint32_t wave_parts = 2;  // units per task (BA_WAVE_SPLIT=3: thirds)
 };
 
 struct ProfScope {  // RAII: times one launch when profiling is on
@@ -137,6 +138,7 @@ hipError_t launch_wave_engine(const RunArgs& a, const Geometry& g);
 bool wave_split_wanted(const RunArgs& a, const Geometry& g);
 uint64_t wave_split_xch_words(const Geometry& g, uint64_t batch);
 uint64_t wave_split_tasks(const Geometry& g, uint64_t batch);
+uint32_t wave_split_parts();
 bool plan_fused(const Geometry& g, FusedPlan& fp);
 hipError_t launch_leaf(const Geometry& g, uint64_t seed, uint64_t gw0, uint32_t W,
                        uint32_t srbase, uint32_t srcnt, uint32_t lbase, const uint64_t* Lm2,

@@ -914,11 +914,16 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM3W_MIN_BLOCKS(N)) void k_om3w(
 // counts.  No wave waits for another (the k_cascade hand-off), and units come
 // from the ctx's dynamic counter: 2 units per task halve the granule a wave
 // takes, so a one-step launch's tail (the SIMD's younger wave running alone
-// after its older partner finished) is about half as long.
+// after its older partner finished) should be about half as long.
+// MEASURED SLOWER (round 3, profiles/r03i_split_ab.log): 98.5 us per 1M-trial
+// launch against k_om3w's 50.1 (thirds: 105 us), bit-identical; the kernel
+// compiles to 238 VGPRs without a bound (46 spills at the 3-block bound)
+// against k_om3w's 170.  Kept as a lab switch (A/B, parity-tested), off by
+// default.
 // xch: [tasks][W][L][L] words; xcnt: [tasks] counters, zero between launches
 // (the last arriver resets its counter).
 // ---------------------------------------------------------------------------
-template <int N>
+template <int N, int P = 2>
 __global__ __launch_bounds__(kWaveThreads, BA_OM3W_MIN_BLOCKS(N)) void k_om3h(
     uint64_t seed, GenSpec gs, uint64_t first_trial, uint64_t batch,
     const uint32_t* __restrict__ faulty, const uint8_t* __restrict__ order,
@@ -926,14 +931,15 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM3W_MIN_BLOCKS(N)) void k_om3h(
     uint64_t* __restrict__ counters, Sink sk, uint64_t* __restrict__ xch,
     uint32_t* __restrict__ xcnt) {
     using G = Om3W<N>;
-    constexpr int L = G::L, C = G::C, W = G::W, NIN = G::NIN, H0 = (L + 1) / 2;
+    constexpr int L = G::L, C = G::C, W = G::W, NIN = G::NIN;
     constexpr uint32_t ME = 3;
+    static_assert(P >= 2 && P <= L, "k_om3h: 2..L parts per task");
     (void)gs;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
     uint64_t* img = lds + (uint64_t)wv * G::words;
     const uint64_t total_words = (batch + 63) / 64;
-    const uint64_t ntasks = (total_words + W - 1) / W, nunits = 2 * ntasks;
+    const uint64_t ntasks = (total_words + W - 1) / W, nunits = (uint64_t)P * ntasks;
     const uint32_t lw_ = lane / C, la = lane - lw_ * C;
     const bool act = lane < (uint32_t)G::LANES;
     const uint32_t lw = act ? lw_ : 0;
@@ -943,9 +949,10 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM3W_MIN_BLOCKS(N)) void k_om3h(
     for (uint64_t u = (uint64_t)blockIdx.x * wpb + wv; u < nunits;) {
         uint32_t next_raw = 0;
         if (sk.tasks != nullptr && lane == 0) next_raw = atomicAdd(sk.tasks, 1u);
-        const uint64_t task = u >> 1;
-        const uint32_t half = (uint32_t)(u & 1u);
-        const uint32_t jb = half ? (uint32_t)H0 : 0u, je = half ? (uint32_t)L : (uint32_t)H0;
+        const uint64_t task = u / P;
+        const uint32_t part = (uint32_t)(u - task * P);
+        // part p runs rounds [p L / P, (p + 1) L / P)
+        const uint32_t jb = part * L / P, je = (part + 1) * L / P;
         const uint64_t w0 = task * W;
         const uint64_t gw0 = (first_trial >> 6) + w0;
         stage_words<N, W>(img + G::oIN, lane, w0, batch, faulty, order);
@@ -964,7 +971,7 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM3W_MIN_BLOCKS(N)) void k_om3h(
             if (act) img[G::oR1 + (lw * L + la + (la >= j1 ? 1u : 0u)) * L + j1] = r1;
         }
         __builtin_amdgcn_wave_barrier();
-        // publish this half's entries R1T[w][col][j1], j1 in [jb, je), col != j1
+        // publish this part's entries R1T[w][col][j1], j1 in [jb, je), col != j1
         uint64_t* xt = xch + task * (uint64_t)(W * L * L);
         const uint32_t nj = je - jb;
         for (uint32_t it = lane; it < (uint32_t)(W * L) * nj; it += 64) {
@@ -972,10 +979,12 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM3W_MIN_BLOCKS(N)) void k_om3h(
             if (row % L != j1) store_sc1(xt + row * L + j1, img[G::oR1 + row * L + j1]);
         }
         drain_stores();
-        if (arrive_last(xcnt + task, 2u, lane)) {
-            const uint32_t ob = half ? 0u : (uint32_t)H0, on = half ? (uint32_t)H0 : (uint32_t)(L - H0);
-            for (uint32_t it = lane; it < (uint32_t)(W * L) * on; it += 64) {
-                const uint32_t row = it / on, j1 = ob + (it - row * on);
+        if (arrive_last(xcnt + task, (uint32_t)P, lane)) {
+            // every other part's entries (all of R1T outside [jb, je))
+            const uint32_t no = (uint32_t)L - nj;
+            for (uint32_t it = lane; it < (uint32_t)(W * L) * no; it += 64) {
+                const uint32_t row = it / no, k = it - row * no;
+                const uint32_t j1 = k < jb ? k : k + nj;
                 if (row % L != j1) img[G::oR1 + row * L + j1] = load_sc1(xt + row * L + j1);
             }
             __builtin_amdgcn_wave_barrier();

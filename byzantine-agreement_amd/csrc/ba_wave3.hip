@@ -12,11 +12,11 @@ bool wave_supported(const Geometry& g) {
 }
 
 // k_om3h: units = 2 per task, dynamic assignment from the ctx's task counter
-template <int N>
+template <int N, int P>
 static hipError_t launch_om3h(const RunArgs& a) {
     using G = Om3W<N>;
     constexpr uint32_t wpb = kWaveThreads / 64;
-    const uint64_t words = (a.batch + 63) / 64, units = 2 * ((words + G::W - 1) / G::W);
+    const uint64_t words = (a.batch + 63) / 64, units = P * ((words + G::W - 1) / G::W);
     uint64_t blocks = (units + wpb - 1) / wpb;
     uint64_t cap = (uint64_t)G::BPC * a.cu_count;
     if (const char* e = getenv("BA_WAVE_MAX_BLOCKS")) {  // tests: force the persistent unit loop
@@ -32,7 +32,7 @@ static hipError_t launch_om3h(const RunArgs& a) {
         if (e != hipSuccess) return e;
     }
     ProfScope ps(a.prof, "k_om3h", a.stream);
-    hipLaunchKernelGGL(k_om3h<N>, dim3((uint32_t)blocks), dim3(kWaveThreads), wpb * G::words * 8,
+    hipLaunchKernelGGL((k_om3h<N, P>), dim3((uint32_t)blocks), dim3(kWaveThreads), wpb * G::words * 8,
                        a.stream, a.seed, a.gen, a.first_trial, a.batch, a.faulty, a.order,
                        a.decisions, a.outcome, a.counters, sk, a.wave_xch, a.wave_cnt);
     return hipGetLastError();
@@ -40,8 +40,12 @@ static hipError_t launch_om3h(const RunArgs& a) {
 
 bool wave_split_wanted(const RunArgs& a, const Geometry& g) {
     const char* e = getenv("BA_WAVE_SPLIT");  // read per call (tests and A/B switch it)
-    return e && atoi(e) != 0 && g.me == 3 && g.n >= 5 && g.n <= 14 && a.gen.faulty_mode == 0 &&
+    return e && (atoi(e) == 2 || atoi(e) == 3 || atoi(e) == 1) && g.me == 3 && g.n >= 5 && g.n <= 14 && a.gen.faulty_mode == 0 &&
            a.gen.order_mode == 0 && a.faulty && a.order;
+}
+uint32_t wave_split_parts() {
+    const char* e = getenv("BA_WAVE_SPLIT");
+    return e && atoi(e) == 3 ? 3u : 2u;  // BA_WAVE_SPLIT=1 or 2: halves; 3: thirds
 }
 uint64_t wave_split_tasks(const Geometry& g, uint64_t batch) {
     const uint64_t C = g.L - 1, W = 64 / C;
@@ -58,7 +62,7 @@ hipError_t launch_wave_engine(const RunArgs& a, const Geometry& g) {
     if (a.wave_xch && a.wave_cnt && a.faulty && a.order) {
         switch (g.n) {
 #define OM3H_CASE(nn) \
-    case nn: return launch_om3h<nn>(a);
+    case nn: return a.wave_parts == 3 ? launch_om3h<nn, 3>(a) : launch_om3h<nn, 2>(a);
             OM3H_CASE(5) OM3H_CASE(6) OM3H_CASE(7) OM3H_CASE(8) OM3H_CASE(9) OM3H_CASE(10)
             OM3H_CASE(11) OM3H_CASE(12) OM3H_CASE(13) OM3H_CASE(14)
 #undef OM3H_CASE

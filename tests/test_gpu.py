@@ -323,16 +323,17 @@ def test_om3_wave_block_generic_vs_oracle(monkeypatch, n, m, f, fmode):
         assert {k: res.counters[k] for k in ocnt} == ocnt, tag
 
 
+@pytest.mark.parametrize("parts", ["2", "3"])
 @pytest.mark.parametrize("n", [5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
-def test_om3_split_halves_vs_oracle(monkeypatch, n):
-    """k_om3h (BA_WAVE_SPLIT=1: each task's first-hop rounds split over two units,
+def test_om3_split_halves_vs_oracle(monkeypatch, n, parts):
+    """k_om3h (BA_WAVE_SPLIT=2 or 3: each task's first-hop rounds split over 2 or 3 units,
     R1 entries exchanged through L2, the second arrival runs roots and epilogue)
     against the oracle on staged (given) inputs: a ragged small batch and a
     mid-size one, with the launch cap at 1 and 2 blocks (every unit through the
     dynamic loop), and twice on one ctx (the arrival counters must be back at
     zero).  The profile proves k_om3h ran."""
     from ba_amd import lib as L
-    monkeypatch.setenv("BA_WAVE_SPLIT", "1")
+    monkeypatch.setenv("BA_WAVE_SPLIT", parts)
     C = n - 2
     W = 64 // C
     for B in (64 * W * 3 + 37, 64 * W * 301 + 5):
