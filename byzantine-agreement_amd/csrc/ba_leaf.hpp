@@ -80,8 +80,14 @@ __device__ __forceinline__ void leaf_block_cols(uint32_t me, uint64_t seed, uint
         constexpr int t0 = grp() * PG, ng = NPAIR - t0 < PG ? NPAIR - t0 : PG;
         P4 c[ng];
         static_for<0, ng>([&](auto g) {
-            c[g()] = P4{pair0 + (uint32_t)LeafSched::step_pair(S, t0 + g()), me, (uint32_t)gw,
-                        (uint32_t)(gw >> 32)};
+            uint32_t cx = pair0 + (uint32_t)LeafSched::step_pair(S, t0 + g());
+#ifndef BA_LEAF_CTR_FOLD
+            // opaque: the round-0 product is one v_mad_u64_u32 of this word, not a
+            // 64-bit add of M0 * pair0 and an SGPR-pair constant M0 * q (21 such
+            // pairs per leaf block held 42 SGPRs and spilled SGPRs to VGPR lanes)
+            asm("" : "+v"(cx));
+#endif
+            c[g()] = P4{cx, me, (uint32_t)gw, (uint32_t)(gw >> 32)};
         });
         philox10_n<ng>(c, (uint32_t)seed, (uint32_t)(seed >> 32));
         static_for<0, ng>([&](auto g) {
