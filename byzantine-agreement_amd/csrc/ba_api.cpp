@@ -646,24 +646,6 @@ static int run_trials_device_impl(ba_ctx* ctx, const ba_params* p, uint64_t batc
                     "%llu B of LDS (n=%u, m_eff=%u)", kWave4MaxN, kFusedMaxDepth, kMaxLeafS,
                     (unsigned long long)kFusedLdsBudget, a.n, a.me);
     if (fused_ok && p->engine != BA_ENGINE_LEVELS) {
-        if (wave_split_wanted(a, g)) {
-            // k_om3h's exchange blocks (ctx scratch, which the WAVE path does not
-            // otherwise use) and arrival counters (zero between calls: zeroed when
-            // grown, reset by each task's last arriver)
-            const uint64_t xb = wave_split_xch_words(g, batch) * sizeof(uint64_t);
-            const uint64_t cb = wave_split_tasks(g, batch) * sizeof(uint32_t);
-            if (xb <= ctx->scratch_budget) {
-                if ((rc = ctx->scratch.grow(xb)) != BA_OK) return rc;
-                if (cb > ctx->casc.bytes) {
-                    if ((rc = ctx->casc.grow(cb)) != BA_OK) return rc;
-                    HIP_TRY(hipMemset(ctx->casc.p, 0, ctx->casc.bytes));
-                    HIP_TRY(hipDeviceSynchronize());  // the launch stream is non-blocking
-                }
-                a.wave_xch = (uint64_t*)ctx->scratch.p;
-                a.wave_cnt = (uint32_t*)ctx->casc.p;
-                a.wave_parts = wave_split_parts();
-            }
-        }
         HIP_TRY(launch_fused(a, g, ge->plan_ok, ge->fp, (const FusedPlan*)ge->fplan.p,
                              (const uint8_t*)ge->sender.p, partials));
         return BA_OK;

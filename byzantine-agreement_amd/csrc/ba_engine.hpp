@@ -47,11 +47,6 @@ struct RunArgs {
     Prof* prof = nullptr;
     const uint64_t* members = nullptr;  // device copy of Geometry::members
     uint32_t cu_count = 256;            // compute units of the ctx device
-    // k_om3h (BA_WAVE_SPLIT=1): the task halves' R1 exchange blocks and arrival
-    // counters (ctx scratch; nullptr = no split)
-    uint64_t* wave_xch = nullptr;
-    uint32_t* wave_cnt = nullptr;
-    uint32_t wave_parts = 2;  // units per task (BA_WAVE_SPLIT=3: thirds)
 };
 
 struct ProfScope {  // RAII: times one launch when profiling is on
@@ -133,12 +128,6 @@ struct FusedPlan {
 bool leaf_supported(const Geometry& g);
 bool wave_supported(const Geometry& g);
 hipError_t launch_wave_engine(const RunArgs& a, const Geometry& g);
-// k_om3h exchange sizes for a batch (0 when the split does not apply: depth
-// other than 3, in-kernel inputs, BA_WAVE_SPLIT unset)
-bool wave_split_wanted(const RunArgs& a, const Geometry& g);
-uint64_t wave_split_xch_words(const Geometry& g, uint64_t batch);
-uint64_t wave_split_tasks(const Geometry& g, uint64_t batch);
-uint32_t wave_split_parts();
 bool plan_fused(const Geometry& g, FusedPlan& fp);
 hipError_t launch_leaf(const Geometry& g, uint64_t seed, uint64_t gw0, uint32_t W,
                        uint32_t srbase, uint32_t srcnt, uint32_t lbase, const uint64_t* Lm2,

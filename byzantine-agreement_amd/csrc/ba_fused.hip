@@ -339,205 +339,6 @@ __global__ __launch_bounds__(kFusedThreads, (S <= 7 ? 4 : 2)) void k_fused(
 }
 
 // ---------------------------------------------------------------------------
-// FUSED, effective depth 3, N generals known at compile time (n=10, m=3 is
-// the BASELINE config).  Same algorithm and LDS image as k_fused, but every
-// index is arithmetic on compile-time constants:
-//   lieutenant ranks 0..L-1 (general = rank+1); level-1 slot y = j1*(L-1) + c
-//   names j1 = y/(L-1) and j2 = c + (c >= j1); the a-th member of prefix
-//   (j1, j2) is a + (a >= lo) + (a >= hi-1), lo/hi = min/max(j1, j2).
-// Relay levels 0 and 1 run as ONE pass: every level-1 slot pair recomputes
-// its parent's level-0 value (one extra Philox call), so no barrier between.
-// The root + per-trial epilogue of a word is done by one wave (no barrier).
-// ---------------------------------------------------------------------------
-template <int N>
-struct Om3 {
-    static constexpr int L = N - 1, S = N - 3;               // lieutenants, leaf members
-    static constexpr int S1 = L * (L - 1), S2 = S1 * (L - 2);  // level-1 / level-2 slots
-    static constexpr int oF = 0, oOB = N, oOO = N + 1, oVAL = N + 2;
-    static constexpr int oL0 = N + 3, oL1 = oL0 + L, oR2 = oL1 + S1, oR1 = oR2 + S2;
-    static constexpr int words = ((oR1 + S1) + 1) & ~1;  // per trial word, 16-B aligned
-    static_assert(2 * L <= S2, "root stash reuses the R2 area");
-};
-
-template <int N>
-__global__ __launch_bounds__(kFusedThreads, ((N - 3) <= 7 ? 4 : 2)) void k_fused3(
-    uint32_t wpb, uint64_t seed, GenSpec gs, uint64_t first_trial, uint64_t batch,
-    const uint32_t* __restrict__ faulty, const uint8_t* __restrict__ order,
-    uint64_t* __restrict__ decisions, uint8_t* __restrict__ outcome,
-    uint64_t* __restrict__ counters, Sink sk) {
-    using G = Om3<N>;
-    constexpr int L = G::L, S = G::S, S1 = G::S1, STRIDE = G::words;
-    constexpr uint32_t ME = 3;
-    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-    __shared__ __attribute__((aligned(16))) unsigned long long blockcnt[16];
-    const uint32_t T = kFusedThreads, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    if (tid < 16) blockcnt[tid] = 0;
-    FUSED_STAMP_INIT();
-    const uint64_t total_words = (batch + 63) / 64;
-    const uint64_t per_block = (total_words + gridDim.x - 1) / gridDim.x;
-    const uint64_t wbeg = (uint64_t)blockIdx.x * per_block;
-    const uint64_t wend = wbeg + per_block < total_words ? wbeg + per_block : total_words;
-    for (uint64_t w0 = wbeg; w0 < wend; w0 += wpb) {
-        const uint32_t nw = (uint32_t)(wend - w0 < wpb ? wend - w0 : wpb);
-        const uint64_t gwg = (first_trial >> 6) + w0;
-        // ---- A: inputs -> bit-sliced words (one wave per word) -------------------
-        for (uint32_t lw = wv; lw < nw; lw += T / 64) {
-            uint64_t* img = lds + lw * STRIDE;
-            const uint64_t i = (w0 + lw) * 64 + lane;
-            const bool valid = i < batch;
-            uint32_t fm = 0, oc = 0;
-            if (valid) {
-                if (gs.faulty_mode == 0) fm = faulty[i];
-                if (gs.order_mode == 0) oc = order[i];
-                gen_trial(N, seed, gs, first_trial + i, fm, oc);
-            }
-            uint64_t mine = 0;
-            static_for<0, N>([&](auto g) {
-                const uint64_t b = __ballot(valid && ((fm >> g()) & 1u));
-                if (lane == g()) mine = b;
-            });
-            const uint64_t ob = __ballot(valid && oc == 1);
-            const uint64_t oo = __ballot(valid && oc == 2);
-            const uint64_t vv = __ballot(valid);
-            if (lane < N) img[G::oF + lane] = mine;
-            if (lane == 0) {
-                img[G::oOB] = ob;
-                img[G::oOO] = oo;
-                img[G::oVAL] = vv;
-            }
-        }
-        __syncthreads();
-        FUSED_STAMP(0);
-        // ---- B: levels 0 and 1 in one pass: item = (word, level-1 slot pair) ------
-        {
-            constexpr uint32_t NP = S1 / 2;  // S1 = L(L-1) is even
-            for (uint32_t it = tid; it < NP * nw; it += T) {
-                const uint32_t lw = it / NP, q = it - lw * NP;
-                uint64_t* img = lds + lw * STRIDE;
-                const uint64_t gw = gwg + lw;
-                const uint64_t F0 = img[G::oF], ob = img[G::oOB];
-                uint32_t x[2], y[2];
-                x[0] = 2 * q;
-                x[1] = 2 * q + 1;
-                y[0] = x[0] / (L - 1);
-                y[1] = x[1] / (L - 1);
-                uint64_t l1a, l1b, p0a, p0b, p1a, p1b;
-                lie_pair(seed, 1, q, gw, l1a, l1b);               // level-1 pair
-                lie_pair(seed, 0, y[0] >> 1, gw, p0a, p0b);       // parent of x0 (level 0)
-                uint64_t L0v[2];
-                L0v[0] = (F0 & ((y[0] & 1) ? p0b : p0a)) | (~F0 & ob);
-                if constexpr ((L - 1) % 2 == 0) {                 // both slots share a parent
-                    L0v[1] = L0v[0];
-                    (void)p1a;
-                    (void)p1b;
-                } else {
-                    lie_pair(seed, 0, y[1] >> 1, gw, p1a, p1b);
-                    L0v[1] = (F0 & ((y[1] & 1) ? p1b : p1a)) | (~F0 & ob);
-                }
-                const uint64_t lie1[2] = {l1a, l1b};
-                static_for<0, 2>([&](auto h) {
-                    const uint64_t fj = img[G::oF + y[h()] + 1];  // sender: lieutenant y
-                    img[G::oL1 + x[h()]] = (fj & lie1[h()]) | (~fj & L0v[h()]);
-                    img[G::oL0 + y[h()]] = L0v[h()];              // identical value from
-                });                                               // every sibling pair
-            }
-        }
-        __syncthreads();
-        FUSED_STAMP(1);
-        // ---- C: leaf blocks, one per (word, level-1 slot) ------------------------
-        for (uint32_t it = tid; it < (uint32_t)S1 * nw; it += T) {
-            const uint32_t lw = it / S1, sr = it - lw * S1;
-            uint64_t* img = lds + lw * STRIDE;
-            const uint64_t gw = gwg + lw;
-            const uint32_t j1 = sr / (L - 1), c = sr - j1 * (L - 1), j2 = c + (c >= j1);
-            const uint32_t lo = j1 < j2 ? j1 : j2, hi = j1 < j2 ? j2 : j1;
-            const uint64_t par = img[G::oL1 + sr];
-            const uint64_t fs = img[G::oF + j2 + 1];  // level-2 sender: j2
-            const uint32_t x0 = sr * S;
-            constexpr int NPD = (S + 1) / 2;
-            uint64_t lw2[2 * NPD];
-            static_for<0, NPD>([&](auto qd) {
-                lie_pair(seed, 2, (x0 >> 1) + qd(), gw, lw2[2 * qd()], lw2[2 * qd() + 1]);
-            });
-            // bitwise select: a ternary here becomes lw2[a + odd], a dynamic index (scratch)
-                const uint64_t oddmask = 0ull - (uint64_t)(x0 & 1u);
-            uint64_t diag[S], Fm[S], R[S];
-            static_for<0, S>([&](auto a) {
-                uint64_t lie;
-                if constexpr (S % 2 == 1) lie = lw2[a()] ^ ((lw2[a()] ^ lw2[a() + 1]) & oddmask);
-                else lie = lw2[a()];
-                diag[a()] = (fs & lie) | (~fs & par);
-                const uint32_t ida = a() + (a() >= lo) + (a() + 1 >= hi);  // member a's rank
-                Fm[a()] = img[G::oF + ida + 1];
-            });
-            leaf_block<S>(ME, seed, gw, sr, diag, Fm, R);
-            static_for<0, S>([&](auto b) { img[G::oR2 + x0 + b()] = R[b()]; });
-        }
-        __syncthreads();
-        FUSED_STAMP(2);
-        // ---- D: R1[j1*(L-1) + b] over L1 and R2 (s = L-1 inputs) -------------------
-        for (uint32_t it = tid; it < (uint32_t)S1 * nw; it += T) {
-            const uint32_t lw = it / S1, y = it - lw * S1;
-            uint64_t* img = lds + lw * STRIDE;
-            const uint32_t j1 = y / (L - 1), b = y - j1 * (L - 1);
-            Count<planes_c(L - 1)> cnt;
-            cnt.add(img[G::oL1 + y]);
-            const uint32_t base = G::oR2 + j1 * (L - 1) * (L - 2);
-            static_for<0, L - 1>([&](auto a) {
-                if (a() == b) return;
-                cnt.add(img[base + a() * (L - 2) + (a() < b ? b - 1 : b)]);
-            });
-            img[G::oR1 + y] = cnt.ge((L - 1) / 2 + 1);
-        }
-        __syncthreads();
-        FUSED_STAMP(3);
-        // ---- E: per wave and word: roots (lanes 0..L-1), then every trial ---------
-        for (uint32_t lw = wv; lw < nw; lw += T / 64) {
-            uint64_t* img = lds + lw * STRIDE;
-            if (lane < (uint32_t)L) {
-                const uint32_t b = lane;
-                Count<planes_c(L)> cnt;
-                cnt.add(img[G::oL0 + b]);
-                static_for<0, L>([&](auto a) {
-                    if (a() == b) return;
-                    cnt.add(img[G::oR1 + a() * (L - 1) + (a() < b ? b - 1 : b)]);
-                });
-                const uint64_t att = cnt.ge(L / 2 + 1);
-                const uint64_t tie = (L & 1) ? 0ull : (cnt.ge(L / 2) & ~att);
-                img[G::oR2 + b] = att;       // R2 is dead after stage D
-                img[G::oR2 + L + b] = tie;
-            }
-            __builtin_amdgcn_wave_barrier();
-            // LDS ops of one wave complete in order: the root words written above
-            // are visible to this wave's reads below without a block barrier
-            const uint64_t w = w0 + lw, i = w * 64 + lane;
-            const bool live = (img[G::oVAL] >> lane) & 1ull;
-            uint32_t A = 0, U = 0, fm = 0;
-            static_for<0, L>([&](auto b) {
-                A |= (uint32_t)((img[G::oR2 + b()] >> lane) & 1ull) << (b() + 1);
-                U |= (uint32_t)((img[G::oR2 + L + b()] >> lane) & 1ull) << (b() + 1);
-            });
-            static_for<0, N>([&](auto g) { fm |= (uint32_t)((img[G::oF + g()] >> lane) & 1ull) << g(); });
-            const uint32_t ob = (uint32_t)(img[G::oOB] >> lane) & 1u;
-            const uint32_t oo = (uint32_t)(img[G::oOO] >> lane) & 1u;
-            const TrialResult r = trial_result(N, ME, fm, oo ? 2u : ob, A, U);
-            if (live) {
-                if (decisions) decisions[i] = r.dec;
-                if (outcome) outcome[i] = (uint8_t)r.out;
-            }
-            wave_counts_add(live, r, blockcnt);
-        }
-        __syncthreads();
-        FUSED_STAMP(5);
-    }
-    // integer sums commute: the block's totals go through the replicated sink
-    // (no k_reduce launch, no single-line atomic hot spot)
-    __syncthreads();
-    if (wv == 0) sink_counters(lane, lane < C_NUM ? blockcnt[lane] : 0, blockIdx.x, gridDim.x, counters, sk);
-    FUSED_STAMP_STORE();
-}
-
-// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 bool leaf_supported(const Geometry& g) {
@@ -649,34 +450,21 @@ hipError_t launch_fused(const RunArgs& a, const Geometry& g, bool plan_ok, const
                         const FusedPlan* d_fp, const uint8_t* d_sender, uint64_t* partials) {
     const uint64_t words = (a.batch + 63) / 64;
     // effective depth 3 or 4 within wave_supported: the WAVE kernels.
-    // BA_FUSED_KIND selects the alternatives for cross-checks: 1 = block
-    // kernel k_fused3 (depth 3), 2 = generic k_fused (trees that fit its plan).
+    // BA_FUSED_KIND=2 runs the generic k_fused on such a tree instead (a
+    // cross-check of two independent kernels in the GPU tests).
     const char* kenv = getenv("BA_FUSED_KIND");
     const int kind = kenv ? atoi(kenv) : 0;
-    if (wave_supported(g) && kind == 0) return launch_wave_engine(a, g);
+    if (wave_supported(g) && kind != 2) return launch_wave_engine(a, g);
     if (!plan_ok) return hipErrorInvalidValue;  // BA_FUSED_KIND forced a kernel this tree lacks
-    // BA_FUSED_KIND=1: the compile-time-specialised block kernel k_fused3
-    const bool spec3 = g.me == 3 && g.n >= 5 && g.n <= 14 && kind != 2;
     // one block per resident slot (occupancy x CUs): each owns an equal run of words
     int occ = 0;
-    if (spec3) {
-        switch (g.n) {
-#define OCC3_CASE(nn) \
-    case nn: (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_fused3<nn>, kFusedThreads, fp.lds_bytes); break;
-            OCC3_CASE(5) OCC3_CASE(6) OCC3_CASE(7) OCC3_CASE(8) OCC3_CASE(9) OCC3_CASE(10)
-            OCC3_CASE(11) OCC3_CASE(12) OCC3_CASE(13) OCC3_CASE(14)
-#undef OCC3_CASE
-            default: return hipErrorInvalidValue;
-        }
-    } else {
-        switch (g.n - g.me) {
+    switch (g.n - g.me) {
 #define OCC_CASE(s) \
     case s: (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_fused<s>, fp.threads, fp.lds_bytes); break;
-            OCC_CASE(2) OCC_CASE(3) OCC_CASE(4) OCC_CASE(5) OCC_CASE(6) OCC_CASE(7)
-            OCC_CASE(8) OCC_CASE(9) OCC_CASE(10) OCC_CASE(11) OCC_CASE(12)
+        OCC_CASE(2) OCC_CASE(3) OCC_CASE(4) OCC_CASE(5) OCC_CASE(6) OCC_CASE(7)
+        OCC_CASE(8) OCC_CASE(9) OCC_CASE(10) OCC_CASE(11) OCC_CASE(12)
 #undef OCC_CASE
-            default: return hipErrorInvalidValue;
-        }
+        default: return hipErrorInvalidValue;
     }
     if (occ < 1) occ = 1;
     uint32_t lds_bytes = fp.lds_bytes;
@@ -695,28 +483,13 @@ hipError_t launch_fused(const RunArgs& a, const Geometry& g, bool plan_ok, const
     const uint32_t blocks = (uint32_t)(words < slots ? words : slots);
     {
         ProfScope ps(a.prof, "k_fused", a.stream);
-        if (spec3) {
-            switch (g.n) {
-#define FUSED3_CASE(nn)                                                                          \
-    case nn:                                                                                     \
-        hipLaunchKernelGGL(k_fused3<nn>, dim3(blocks), dim3(kFusedThreads), lds_bytes, a.stream, \
-                           fp.wpb, a.seed, a.gen, a.first_trial, a.batch, a.faulty, a.order,     \
-                           a.decisions, a.outcome, a.counters, a.sink);                         \
-        break;
-                FUSED3_CASE(5) FUSED3_CASE(6) FUSED3_CASE(7) FUSED3_CASE(8) FUSED3_CASE(9)
-                FUSED3_CASE(10) FUSED3_CASE(11) FUSED3_CASE(12) FUSED3_CASE(13) FUSED3_CASE(14)
-#undef FUSED3_CASE
-                default: return hipErrorInvalidValue;
-            }
-        } else {
-            switch (g.n - g.me) {
+        switch (g.n - g.me) {
 #define FUSED_CASE(s) \
     case s: launch_fused_s<s>(fp, d_fp, blocks, lds_bytes, a, d_sender, partials); break;
-                FUSED_CASE(2) FUSED_CASE(3) FUSED_CASE(4) FUSED_CASE(5) FUSED_CASE(6) FUSED_CASE(7)
-                FUSED_CASE(8) FUSED_CASE(9) FUSED_CASE(10) FUSED_CASE(11) FUSED_CASE(12)
+            FUSED_CASE(2) FUSED_CASE(3) FUSED_CASE(4) FUSED_CASE(5) FUSED_CASE(6) FUSED_CASE(7)
+            FUSED_CASE(8) FUSED_CASE(9) FUSED_CASE(10) FUSED_CASE(11) FUSED_CASE(12)
 #undef FUSED_CASE
-                default: return hipErrorInvalidValue;
-            }
+            default: return hipErrorInvalidValue;
         }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;

@@ -285,11 +285,11 @@ OM3_CASES = [(5, 3, 1, 1), (5, 4, 2, 1), (6, 3, 1, 2), (7, 3, 2, 1), (8, 3, 3, 1
 
 @pytest.mark.parametrize("n,m,f,fmode", OM3_CASES)
 def test_om3_wave_block_generic_vs_oracle(monkeypatch, n, m, f, fmode):
-    """k_om3w (default), k_om3q (BA_WAVE_KIND=2), k_fused3 (BA_FUSED_KIND=1) and
-    k_fused (=2) against the oracle, over every synthetic-input path of the WAVE
+    """k_om3w (default) and the generic block kernel k_fused (BA_FUSED_KIND=2)
+    against the oracle, over every synthetic-input path of the WAVE
     kernels' branch-free generator (f <= 2, 3, <= 6 and the generic fallback;
     random / exact / given faulty sets), a ragged batch, and the persistent
-    loops (BA_WAVE_MAX_BLOCKS=1: one block walks every task group)."""
+    loop (BA_WAVE_MAX_BLOCKS=1: one block walks every task)."""
     from ba_amd import lib as L
     B = 64 * 8 * 5 + 37
     if fmode == 0:
@@ -304,10 +304,8 @@ def test_om3_wave_block_generic_vs_oracle(monkeypatch, n, m, f, fmode):
                   L.ORDER_CONST, order_value=1, first_trial=64 * 77)
         ref = oracle_c.run(n, m, B, **kw)
     od, oo, ocnt = ref
-    for kind, cap, wk in (("0", None, "0"), ("0", "1", "0"), ("0", None, "2"), ("0", "1", "2"),
-                          ("1", None, "0"), ("2", None, "0")):
+    for kind, cap in (("0", None), ("0", "1"), ("2", None)):
         monkeypatch.setenv("BA_FUSED_KIND", kind)
-        monkeypatch.setenv("BA_WAVE_KIND", wk)
         if cap:
             monkeypatch.setenv("BA_WAVE_MAX_BLOCKS", cap)
         else:
@@ -317,61 +315,19 @@ def test_om3_wave_block_generic_vs_oracle(monkeypatch, n, m, f, fmode):
             res = e.run(n, m, B, engine=L.ENGINE_FUSED, **kw)
         finally:
             e.close()
-        tag = f"kind={kind} wave={wk} cap={cap} n={n} m={m} f={f} fmode={fmode}"
+        tag = f"kind={kind} cap={cap} n={n} m={m} f={f} fmode={fmode}"
         same(res.decisions, od, "decisions " + tag)
         same(res.outcome, oo, "outcome " + tag)
         assert {k: res.counters[k] for k in ocnt} == ocnt, tag
 
 
-@pytest.mark.parametrize("parts", ["2", "3"])
-@pytest.mark.parametrize("n", [5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
-def test_om3_split_halves_vs_oracle(monkeypatch, n, parts):
-    """k_om3h (BA_WAVE_SPLIT=2 or 3: each task's first-hop rounds split over 2 or 3 units,
-    R1 entries exchanged through L2, the second arrival runs roots and epilogue)
-    against the oracle on staged (given) inputs: a ragged small batch and a
-    mid-size one, with the launch cap at 1 and 2 blocks (every unit through the
-    dynamic loop), and twice on one ctx (the arrival counters must be back at
-    zero).  The profile proves k_om3h ran."""
-    from ba_amd import lib as L
-    monkeypatch.setenv("BA_WAVE_SPLIT", parts)
-    C = n - 2
-    W = 64 // C
-    for B in (64 * W * 3 + 37, 64 * W * 301 + 5):
-        rng = np.random.default_rng(n * 7 + B)
-        fm = (rng.integers(0, 1 << n, B, dtype=np.uint64) & rng.integers(0, 1 << n, B, dtype=np.uint64)
-              & rng.integers(0, 1 << n, B, dtype=np.uint64)).astype(np.uint32)
-        oc = rng.choice([0, 1, 2], B).astype(np.uint8)
-        od, oo, ocnt = oracle_c.run(n, 3, B, seed=11, faulty=fm, order=oc, first_trial=64 * 5)
-        for cap in (None, "1", "2"):
-            if cap:
-                monkeypatch.setenv("BA_WAVE_MAX_BLOCKS", cap)
-            else:
-                monkeypatch.delenv("BA_WAVE_MAX_BLOCKS", raising=False)
-            e = L.Engine(0)
-            try:
-                e.profile(True)
-                for rep in range(2):
-                    res = e.run(n, 3, B, seed=11, faulty=fm, order=oc, first_trial=64 * 5,
-                                engine=L.ENGINE_FUSED)
-                    tag = f"n={n} B={B} cap={cap} rep={rep}"
-                    same(res.decisions, od, "decisions " + tag)
-                    same(res.outcome, oo, "outcome " + tag)
-                    assert {k: res.counters[k] for k in ocnt} == ocnt, tag
-                assert "k_om3h" in e.profile_read(), "k_om3h did not run"
-            finally:
-                e.close()
-
-
-@pytest.mark.parametrize("kind", ["0", "2"])
 @pytest.mark.parametrize("n,B", [(10, 64 * 8 * 700 + 5), (13, 64 * 5 * 600 + 63), (7, 64 * 16 * 300)])
-def test_om3_mid_batches_vs_oracle(monkeypatch, engine, n, B, kind):
-    """Depth-3 WAVE kernels at mid-size batches: k_om3w (default: several tasks per
-    wave in its persistent loop) and k_om3q (BA_WAVE_KIND=2: several tasks per block
-    group, tpg = ceil(tasks / CUs) = 2..3, ragged last group), staged and drawn
-    inputs, against the oracle."""
+def test_om3_mid_batches_vs_oracle(engine, n, B):
+    """The depth-3 WAVE kernel k_om3w at mid-size batches (several tasks per wave in
+    its persistent loop, ragged last task), staged and drawn inputs, against the
+    oracle."""
     import torch
     from ba_amd import lib as L
-    monkeypatch.setenv("BA_WAVE_KIND", kind)
     kw = dict(seed=0xC0FFEE + n, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1,
               order_mode=L.ORDER_RANDOM, first_trial=64 * 11)
     od, oo, ocnt = oracle_c.run(n, 3, B, **kw)

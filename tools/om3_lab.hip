@@ -9,6 +9,7 @@
 #include "../byzantine-agreement_amd/csrc/ba_wave3.hip"
 #include "../byzantine-agreement_amd/csrc/ba_wave4.hip"
 #include "../byzantine-agreement_amd/csrc/ba_levels.hip"
+#include "lab_kernels.hpp"
 
 #include <cstdio>
 #include <cstdlib>

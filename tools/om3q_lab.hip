@@ -7,6 +7,7 @@
 #include "../byzantine-agreement_amd/csrc/ba_levels.hip"
 #include "../byzantine-agreement_amd/csrc/ba_wave4.hip"
 #include "../byzantine-agreement_amd/csrc/ba_fused.hip"
+#include "lab_kernels.hpp"
 
 #include <algorithm>
 #include <cstdio>
