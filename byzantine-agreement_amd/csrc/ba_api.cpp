@@ -219,6 +219,7 @@ struct ba_ctx {
     DevBuf scratch, partials, io_faulty, io_order, io_table, io_poll, io_dec, io_out, io_cnt;
     DevBuf sink;  // counter sink replicas (zeroed once; kernels leave them zero)
     DevBuf casc;  // k_cascade's fan-in counters (zeroed when grown; kernels leave them zero)
+    uint64_t casc_epoch = 0x5eed0000;  // k_cascade check builds: one tag per launch
     std::map<uint64_t, std::unique_ptr<GeoEntry>> geos;
     Prof prof;
     std::map<std::string, ProfTotal> prof_totals;
@@ -584,33 +585,51 @@ static bool use_cascade(ba_ctx* ctx, const Geometry& g) {
     return !off && ctx->leaf_fusion && leaf_supported(g) && g.me >= 3 && cascade_supported(g);
 }
 
-static int run_cascade(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge) {
+// BA_CASC_CHECK (tests only, read per call): 1 = the cascade's check build
+// (epoch tags beside every hand-off word, mismatches counted into
+// BA_C_CHECK_MISMATCH), 2 = the same with one stale tag injected.
+static uint32_t cascade_check_mode(const Geometry& g) {
+    const char* e = getenv("BA_CASC_CHECK");
+    const int v = e ? atoi(e) : 0;
+    return (v == 1 || v == 2) && cascade_check_supported(g) ? (uint32_t)v : 0u;
+}
+
+// job.h != 0 (the subtree split): one chunk (`whole`), no counters.
+static int run_cascade(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge, CascJob job = CascJob{}) {
     const Geometry& g = ge->g;
-    const uint64_t per_word = cascade_scratch_words_per_word(g) * sizeof(uint64_t);
+    job.check = job.h ? 0u : cascade_check_mode(g);
+    // per trial word: R_1 .. R_{me-2} (twice with check tags) and the fan-in
+    // counters, one 128-B line each -- both count against the scratch budget
+    const uint64_t r_bytes = cascade_scratch_words_per_word(g) * sizeof(uint64_t) * (job.check ? 2 : 1);
+    const uint64_t c_bytes = cascade_counters_per_word(g) * 128;
     const uint64_t words = (a.batch + 63) / 64;
     uint64_t max_level = 0;
     for (uint32_t k = 0; k + 2 <= g.me; ++k) max_level = g.S[k] > max_level ? g.S[k] : max_level;
-    uint64_t chunk = ctx->scratch_budget / (per_word ? per_word : 1);
+    uint64_t chunk = ctx->scratch_budget / (r_bytes + c_bytes);
     const uint64_t idx_cap = (1ull << 31) / (max_level + 1);  // 32-bit slot indices in the kernel
     if (chunk > idx_cap) chunk = idx_cap;
     if (chunk > words) chunk = words;
-    if (chunk == 0)
-        return fail(BA_ETOOBIG, "one 64-trial word needs %llu bytes of scratch (budget %zu)",
-                    (unsigned long long)per_word, ctx->scratch_budget);
+    if (chunk == 0 || (job.h && chunk < words))
+        return fail(BA_ETOOBIG, "%llu 64-trial words need %llu bytes of scratch and counters each "
+                    "(budget %zu%s)", (unsigned long long)words, (unsigned long long)(r_bytes + c_bytes),
+                    ctx->scratch_budget, job.h ? ", one chunk required: split the batch" : "");
     int rc;
-    if ((rc = ctx->scratch.grow(chunk * per_word)) != BA_OK) return rc;
-    const size_t cbytes = chunk * cascade_counters_per_word(g) * 128;
+    if ((rc = ctx->scratch.grow(chunk * r_bytes)) != BA_OK) return rc;
+    const size_t cbytes = chunk * c_bytes;
     if (cbytes > ctx->casc.bytes) {
+        // zeroed on the launch stream, ahead of the first kernel that uses them
+        // (kernels leave them zero); a graph capture must follow an eager call
+        // of at least its size (include/ba.h)
         if ((rc = ctx->casc.grow(cbytes)) != BA_OK) return rc;
-        HIP_TRY(hipMemset(ctx->casc.p, 0, ctx->casc.bytes));  // kernels leave them zero
-        HIP_TRY(hipDeviceSynchronize());  // the launch stream is non-blocking
+        HIP_TRY(hipMemsetAsync(ctx->casc.p, 0, ctx->casc.bytes, a.stream));
     }
     for (uint64_t w0 = 0; w0 < words; w0 += chunk) {
         const uint64_t wn = (words - w0) < chunk ? (words - w0) : chunk;
         const uint64_t trial0 = w0 * 64;
         const uint64_t nt = (a.batch - trial0) < wn * 64 ? (a.batch - trial0) : wn * 64;
+        job.epoch = ++ctx->casc_epoch;
         HIP_TRY(launch_cascade(a, g, (const uint8_t*)ge->sender.p, (uint64_t*)ctx->scratch.p,
-                               (uint32_t*)ctx->casc.p, trial0, nt));
+                               (uint32_t*)ctx->casc.p, trial0, nt, job));
     }
     return BA_OK;
 }
@@ -728,6 +747,14 @@ static int subtree_votes_impl(ba_ctx* ctx, const ba_params* p, uint64_t batch, u
     GeoEntry* ge = geometry(ctx, a.n, a.me, &rc);
     if (!ge) return rc;
     a.members = (const uint64_t*)ge->members.p;
+    if (use_cascade(ctx, ge->g) && cascade_range_supported(ge->g, level)) {
+        CascJob cj;  // the one-launch cascade over the range's level-(me-3) units
+        cj.h = level;
+        cj.ub = j_begin;
+        cj.ue = j_end;
+        cj.votes = d_votes;
+        return run_cascade(ctx, a, ge, cj);
+    }
     LevelsJob job;
     job.root = false;
     job.h = level;

@@ -21,13 +21,26 @@
 //   parent, and so on up to q = 0: the root majorities (tie -> undefined) and
 //   the quorum epilogue of the word (ba.py:197-255, wave_epilogue).
 //
-// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, table row 1):
-// results are stored write-through (sc1: relaxed agent-scope atomic stores),
-// the storing wave drains vmcnt, then ONE lane adds to the parent's counter
-// (agent scope); the wave whose add returns the last count reads the children
-// with sc1 loads only, after its add returned.  Counters sit on 128-B lines of
-// their own; the last arriver resets its counter, so the buffer is zero between
-// calls (zeroed once when the ctx allocates it).
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): results are
+// stored write-through (sc1: relaxed agent-scope atomic stores), the storing
+// wave drains vmcnt, then ONE lane per unit adds to the parent's counter (agent
+// scope); the wave whose add returns the last count takes an agent-scope
+// acquire (buffer_inv sc1: the guide's "Consumer, always" form, valid at any
+// number of workgroups per CU) and reads the children with sc1 loads.  The
+// children of one parent sit on 128-B lines of their own (each sigma's child
+// block is padded to whole lines, casc_pad), so no line a reader pulls in is
+// ever shared with a hand-off that is still being written.  Counters sit on
+// 128-B lines of their own; the last arriver resets its counter, so the buffer
+// is zero between calls (zeroed once when the ctx allocates it).
+//
+// CHECK (test builds, BA_CASC_CHECK=1|2): every R store also stores a tag of
+// the call's epoch (sc1, parallel array), every child load also loads its tag,
+// and mismatches are counted into counter slot BA_C_CHECK_MISMATCH; =2 makes
+// the first unit of the launch store a stale tag (the detector must fire once).
+//
+// Range mode (a.h = 1 or 2; the subtree split, ba_split_votes_device): the
+// units are the level-Q slots below the h-hop subtrees [ub, ue); the step at
+// level h writes its majorities to the vote array and the fan-in stops there.
 //
 // Bit-identical to the LEVELS pipeline: same lie keying (level, global slot
 // pair, global word), same majorities and epilogue.
@@ -40,6 +53,7 @@
 #define BA_PHILOX_SKEYS 1
 #endif
 #include "ba_wave.hpp"
+#include "../../include/ba.h"  // BA_C_CHECK_MISMATCH
 
 namespace ba {
 
@@ -58,19 +72,27 @@ struct CascArgs {
     uint64_t first_trial;  // global index of the chunk's trial 0
     uint64_t ntrials;      // trials of this chunk
     uint32_t W;            // words of this chunk
-    uint32_t units;        // W * |L_Q|
+    uint32_t units;        // W * rr
+    uint32_t rr;           // units (level-Q slots) per word: |L_Q|, or the range's share
+    uint32_t rho0;         // first level-Q slot of the range (0: whole tree)
     const uint32_t* faulty;  // chunk-relative (GIVEN), or nullptr
     const uint8_t* order;
     const uint8_t* sender;   // Geometry::sender
     uint32_t snd_off[kCascMaxLevels];
     const uint64_t* members;  // level me-2 leaf-block member ids, 5 bits each
-    uint64_t* R[kCascMaxLevels];  // R_k, k = 1..me-2: [W][|L_k|] (word-major)
+    uint64_t* R[kCascMaxLevels];    // R_k, k = 1..me-2: [W][groups][casc_pad] (casc_addr)
+    uint64_t* tag[kCascMaxLevels];  // CHECK: the same layout, epoch tags
+    uint64_t epoch;                 // CHECK: this launch's tag
+    uint32_t inject;                // CHECK: 1 = unit 0 stores a stale tag (detector test)
     uint32_t* cnt;                // counters [..] x kCascCounterStride
     uint32_t cnt_off[kCascMaxLevels];  // level k (0..Q-1) counters of word w at cnt_off[k] + w*|L_k|;
                                        // cnt_off[Q]: the word's root counter at cnt_off[Q] + w
+    uint32_t h;           // range mode: the vote level (1 or 2); 0 = whole tree
+    uint32_t ub;          // range mode: first h-hop subtree of the range
+    uint64_t* votes;      // range mode: [(u - ub)(L - h) + c][W]
     uint64_t* decisions;  // chunk-relative
     uint8_t* outcome;
-    uint64_t* counters;
+    uint64_t* counters;   // nullptr in range mode
     Sink sk;
 };
 
@@ -80,17 +102,37 @@ constexpr uint32_t casc_sz(int L, int k) {
     for (int i = 0; i <= k; ++i) p *= (uint32_t)(L - i);
     return p;
 }
+// R_k (k >= 1) is stored in groups: the children of one level k-1 slot's
+// children, i.e. one step's whole input block (L-k+1)(L-k) words (k = 1: the
+// word's root step), each group padded to whole 128-B lines.
+constexpr uint32_t casc_grp(int L, int k) { return (uint32_t)((L - k + 1) * (L - k)); }
+constexpr uint32_t casc_pad(int L, int k) { return (casc_grp(L, k) + 15u) & ~15u; }
+constexpr uint32_t casc_ngrp(int L, int k) { return k >= 2 ? casc_sz(L, k - 2) : 1u; }
+constexpr uint64_t casc_level_words(int L, int k) { return (uint64_t)casc_ngrp(L, k) * casc_pad(L, k); }
 
 template <int N, int ME>
 struct Casc {
     static constexpr int L = N - 1, S = N - ME, G = S + 1, GP = G + 1, GPW = 64 / G;
     static constexpr int Q = ME - 3, NIN = N + 3;
     static constexpr uint32_t sz(int k) { return casc_sz(L, k); }
+    // word w's level-k slot x (k >= 1) in R_k / tag_k
+    template <int k>
+    static __device__ __forceinline__ uint64_t addr(uint32_t w, uint32_t x) {
+        constexpr uint32_t gk = casc_grp(L, k);
+        const uint32_t grp = x / gk;
+        return ((uint64_t)w * casc_ngrp(L, k) + grp) * casc_pad(L, k) + (x - grp * gk);
+    }
     static constexpr int tr_words = GPW * G * GP;  // per wave: [unit][receiver][sender] transpose
+    // fewest units per word: a range of one h-hop subtree with h = Q (L - Q
+    // level-Q slots), or the whole |L_Q| at Q = 0
+    static constexpr uint32_t rr_min = Q >= 1 ? (uint32_t)(L - Q) : casc_sz(L, Q);
     // words a block's 4 * GPW units can span, and their input planes
-    static constexpr uint32_t nw_max = (kCascWaves * GPW + casc_sz(L, Q) - 1) / casc_sz(L, Q) + 1;
+    static constexpr uint32_t nw_max = (kCascWaves * GPW + rr_min - 1) / rr_min + 1;
     static constexpr uint32_t planes_words = (nw_max * NIN + 1u) & ~1u;
 };
+
+// CHECK: the tag stored beside every R word of one launch
+__device__ __forceinline__ uint64_t casc_tag(uint64_t epoch) { return epoch | (~epoch << 32); }
 
 __device__ __forceinline__ uint64_t sel64(uint64_t f, uint64_t a, uint64_t b) { return (f & a) | (~f & b); }
 
@@ -228,13 +270,34 @@ __device__ __forceinline__ uint64_t relay_slots(const CascArgs& a, const uint64_
     return r;
 }
 
+// The arrival that completes a counter: an agent-scope acquire before the
+// children are read (BA_CASC_ACQUIRE=0: sc1 loads alone, A/B only).
+#ifndef BA_CASC_ACQUIRE
+#define BA_CASC_ACQUIRE 1
+#endif
+__device__ __forceinline__ void casc_acquire() {
+#if BA_CASC_ACQUIRE
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+}
+
+// R store of one hand-off word (+ its tag in CHECK builds): write-through
+template <int N, int ME, int k, bool CHECK>
+__device__ __forceinline__ void casc_put(const CascArgs& a, uint32_t w, uint32_t x, uint64_t v,
+                                         bool stale = false) {
+    const uint64_t i = Casc<N, ME>::template addr<k>(w, x);
+    store_sc1(a.R[k] + i, v);
+    if constexpr (CHECK) store_sc1(a.tag[k] + i, casc_tag(stale ? a.epoch - 1 : a.epoch));
+}
+
 // Step q for sigma (level q-1 slot s; q = 0: the word's roots), run by one
 // whole wave, lane r = receiver index among the K = L - q lieutenants not in
 // sigma.  in: the word's input planes (LDS); scr: the wave's LDS scratch.
-template <int N, int ME, int q>
+// mm: CHECK builds' per-lane count of child tags that were not this launch's.
+template <int N, int ME, int q, bool CHECK>
 __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in, uint64_t* scr,
                                           uint32_t lane, uint32_t w, uint32_t s, uint64_t gw,
-                                          TrialCounts& tc) {
+                                          TrialCounts& tc, uint32_t& mm) {
     using C = Casc<N, ME>;
     constexpr int L = C::L, K = L - q;
     const bool act = lane < (uint32_t)K;
@@ -244,19 +307,27 @@ __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in,
     if constexpr (q > 0) unrank_path<L, q - 1>(s, path, srt);
     const uint64_t lq = relay_slots<N, q, K, 64>(a, in, scr, lane, true, s, s * (uint32_t)K, path, gw);
     // R_{q+1}[sigma.j.r], j != r: child c = r - (r > j) of level-q slot s*K + j
-    const uint64_t* Rc = a.R[q + 1] + (uint64_t)w * C::sz(q + 1);
+    // (sigma's child block: one padded group of R_{q+1})
     uint64_t cv[K - 1];
     static_for<0, K - 1>([&](auto jj) {
         const uint32_t j = (uint32_t)jj() + ((uint32_t)jj() >= r ? 1u : 0u);
-        const uint32_t idx = (s * (uint32_t)K + j) * (uint32_t)(K - 1) + r - (r > j ? 1u : 0u);
-        cv[jj()] = act ? load_sc1(Rc + idx) : 0ull;
+        const uint32_t x = (s * (uint32_t)K + j) * (uint32_t)(K - 1) + r - (r > j ? 1u : 0u);
+        const uint64_t i = C::template addr<q + 1>(w, x);
+        cv[jj()] = act ? load_sc1(a.R[q + 1] + i) : 0ull;
+        if constexpr (CHECK) {
+            if (act && load_sc1(a.tag[q + 1] + i) != casc_tag(a.epoch)) ++mm;
+        }
     });
     Csa<planes_c(K)> cnt;
     cnt.template add<0>(lq);
     static_for<0, K - 1>([&](auto jj) { cnt.template add<jj() + 1>(cv[jj()]); });
     if constexpr (q > 0) {
         const uint64_t rq = cnt.template ge<K, K / 2 + 1>();  // inner tie -> non-attack
-        if (act) store_sc1(a.R[q] + (uint64_t)w * C::sz(q) + s * (uint32_t)K + r, rq);
+        if (a.h == (uint32_t)q) {  // range mode: sigma's majorities are votes, the fan-in stops
+            if (act) a.votes[((uint64_t)(s - a.ub) * K + r) * a.W + w] = rq;
+            return;
+        }
+        if (act) casc_put<N, ME, q, CHECK>(a, w, s * (uint32_t)K + r, rq);
         drain_stores();
         // arrive at sigma's parent (level q-2), or at the word's root counter
         constexpr uint32_t up_fan = (uint32_t)(L - (q - 1));  // children of a level q-2 slot
@@ -266,7 +337,10 @@ __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in,
             c = a.cnt + (uint64_t)(a.cnt_off[q - 2] + w * C::sz(q - 2) + ps) * kCascCounterStride;
         else
             c = a.cnt + (uint64_t)(a.cnt_off[C::Q] + w) * kCascCounterStride;
-        if (arrive_last(c, up_fan, lane)) casc_step<N, ME, q - 1>(a, in, scr, lane, w, ps, gw, tc);
+        if (arrive_last(c, up_fan, lane)) {
+            casc_acquire();
+            casc_step<N, ME, q - 1, CHECK>(a, in, scr, lane, w, ps, gw, tc, mm);
+        }
     } else {
         constexpr int NIN = C::NIN;
         const uint64_t att = cnt.template ge<K, K / 2 + 1>();
@@ -298,27 +372,28 @@ __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in,
 // m=5 at 1024 instances, at 207 VGPRs = 2 waves per SIMD.)
 // DIAG (lab only, tools/casc_lab.py, BA_CASC_DIAG; wrong results): 2 = no
 // fan-in (units only), 4 = arrivals but no steps.  The product uses 0.
-template <int N, int ME, int DIAG = 0>
+template <int N, int ME, int DIAG = 0, bool CHECK = false>
 __global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
     using C = Casc<N, ME>;
     constexpr int L = C::L, S = C::S, G = C::G, GP = C::GP, GPW = C::GPW, NIN = C::NIN, Q = C::Q;
-    constexpr uint32_t R = C::sz(Q);  // units per word
     constexpr int NPD = (S + 1) / 2;
     constexpr uint32_t fan = (uint32_t)(L - Q);  // children of a level Q-1 slot (or of the root)
     using RP = RelayPlan<N, Q + 1, G>;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t RR = a.rr;  // units per word
     const uint32_t u0 = blockIdx.x * kCascWaves * GPW;
-    const uint32_t wfirst = u0 / R, nw = (min(u0 + kCascWaves * GPW, a.units) - 1u) / R - wfirst + 1u;
+    const uint32_t wfirst = u0 / RR, nw = (min(u0 + kCascWaves * GPW, a.units) - 1u) / RR - wfirst + 1u;
     uint64_t* planes = lds;  // [nw][NIN]
     uint64_t* tr = lds + C::planes_words + wv * (uint32_t)C::tr_words;
     const uint64_t gw0 = a.first_trial >> 6;
     TrialCounts tc;
+    uint32_t mm = 0;  // CHECK: stale child tags seen by this lane
     const uint32_t g = lane / G, x = lane - g * G;
     const uint32_t u = u0 + wv * GPW + g;
     const bool act = g < (uint32_t)GPW && u < a.units;
     const uint32_t uu = act ? u : u0;
-    const uint32_t w = uu / R, rho = uu - w * R;
+    const uint32_t w = uu / RR, rho = a.rho0 + (uu - w * RR);
     const uint64_t gw = gw0 + w;
     const uint32_t sr = rho * (uint32_t)G + x;  // the lane's level me-2 slot
     const uint32_t gg = act ? g : 0u;
@@ -364,7 +439,8 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
         const uint64_t* col = tr + (gg * G + x) * GP;
         Csa<planes_c(G)> cnt;
         static_for<0, G>([&](auto b) { cnt.template add<b()>(col[b()]); });
-        store_sc1(a.R[ME - 2] + (uint64_t)w * C::sz(ME - 2) + sr, cnt.template ge<G, G / 2 + 1>());
+        casc_put<N, ME, ME - 2, CHECK>(a, w, sr, cnt.template ge<G, G / 2 + 1>(),
+                                       CHECK && a.inject && u == 0 && x == 0);
     }
     __builtin_amdgcn_wave_barrier();
     if constexpr ((DIAG & 2) == 0) {
@@ -384,22 +460,32 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         uint64_t lastmask = (DIAG & 4) ? 0ull : __ballot(last);
+        if (lastmask) casc_acquire();
         while (lastmask) {  // wave-uniform: every lane runs each completed parent's step
             const uint32_t b = (uint32_t)__builtin_ctzll(lastmask);
             lastmask &= lastmask - 1;
             const uint32_t wb = (uint32_t)__builtin_amdgcn_readlane((int)w, (int)b);
             const uint32_t rb = (uint32_t)__builtin_amdgcn_readlane((int)rho, (int)b);
-            casc_step<N, ME, Q>(a, planes + (wb - wfirst) * NIN, tr, lane, wb,
-                                Q >= 1 ? rb / fan : 0u, gw0 + wb, tc);
+            casc_step<N, ME, Q, CHECK>(a, planes + (wb - wfirst) * NIN, tr, lane, wb,
+                                       Q >= 1 ? rb / fan : 0u, gw0 + wb, tc, mm);
         }
     }
-    wave_flush(tc, lane, wv, kCascWaves, a.counters, a.sk, false);
+    if constexpr (CHECK) {
+        uint32_t t = mm;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+        if (lane == 0 && t != 0 && a.counters)
+            atomicAdd((unsigned long long*)(a.counters + BA_C_CHECK_MISMATCH), (unsigned long long)t);
+    }
+    wave_flush(tc, lane, wv, kCascWaves, a.counters, a.sk, a.counters == nullptr);
 }
 
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 #define BA_CASC_SHAPES(X) X(16, 5) X(16, 4) X(16, 3) X(10, 3) X(9, 4) X(8, 5)
+// CHECK builds (tests only): depth 5 at two fan-outs, and a root-only cascade
+#define BA_CASC_CHECK_SHAPES(X) X(16, 5) X(8, 5) X(10, 3)
 
 bool cascade_supported(const Geometry& g) {
 #define BA_CASC_OK(nn, mm) if (g.n == nn && g.me == mm) return true;
@@ -416,25 +502,33 @@ uint64_t cascade_counters_per_word(const Geometry& g) {
     return c;
 }
 
+// R_1 .. R_{me-2} of one word, each step's child block padded to whole lines
 uint64_t cascade_scratch_words_per_word(const Geometry& g) {
     uint64_t s = 0;
-    for (uint32_t k = 1; k + 2 <= g.me; ++k) s += g.S[k];
+    for (uint32_t k = 1; k + 2 <= g.me; ++k) s += casc_level_words((int)g.L, (int)k);
     return s;
 }
 
-template <int N, int ME, int DIAG = 0>
-static hipError_t launch_cascade_t(CascArgs& ca, uint32_t cu_count, hipStream_t st) {
+// the subtree split through the cascade: h-hop subtrees need h <= me-3 (the
+// vote step is a fan-in step, not the units' own level)
+bool cascade_range_supported(const Geometry& g, uint32_t h) {
+    return cascade_supported(g) && (h == 1 || h == 2) && h + 3 <= g.me;
+}
+
+template <int N, int ME, int DIAG = 0, bool CHECK = false>
+static hipError_t launch_cascade_t(CascArgs& ca, hipStream_t st) {
     using C = Casc<N, ME>;
     constexpr uint32_t per_block = kCascWaves * C::GPW;
-    const uint32_t iters = (ca.units + per_block - 1) / per_block;
+    const uint32_t blocks = (ca.units + per_block - 1) / per_block;
     const size_t lds = (size_t)(C::planes_words + kCascWaves * C::tr_words) * sizeof(uint64_t);
-    const uint32_t blocks = iters;
-    hipLaunchKernelGGL((k_cascade<N, ME, DIAG>), dim3(blocks ? blocks : 1), dim3(64 * kCascWaves), lds, st, ca);
+    hipLaunchKernelGGL((k_cascade<N, ME, DIAG, CHECK>), dim3(blocks ? blocks : 1), dim3(64 * kCascWaves), lds,
+                       st, ca);
     return hipGetLastError();
 }
 
 hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_sender,
-                          uint64_t* scratch, uint32_t* d_cnt, uint64_t trial0, uint64_t ntrials) {
+                          uint64_t* scratch, uint32_t* d_cnt, uint64_t trial0, uint64_t ntrials,
+                          const CascJob& job) {
     CascArgs ca{};
     const uint64_t W = (ntrials + 63) / 64;
     ca.seed = a.seed;
@@ -442,7 +536,16 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
     ca.first_trial = a.first_trial + trial0;
     ca.ntrials = ntrials;
     ca.W = (uint32_t)W;
-    ca.units = (uint32_t)(W * g.S[g.me - 3]);
+    const uint64_t RQ = g.S[g.me - 3];
+    if (job.h == 0) {
+        ca.rr = (uint32_t)RQ;
+        ca.rho0 = 0;
+    } else {  // level-Q slots below the h-hop subtrees [ub, ue)
+        const uint64_t per = RQ / g.S[job.h - 1];
+        ca.rr = (uint32_t)((job.ue - job.ub) * per);
+        ca.rho0 = (uint32_t)(job.ub * per);
+    }
+    ca.units = (uint32_t)(W * ca.rr);
     ca.faulty = a.faulty ? a.faulty + trial0 : nullptr;
     ca.order = a.order ? a.order + trial0 : nullptr;
     ca.sender = d_sender;
@@ -450,10 +553,14 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
         ca.snd_off[k] = (uint32_t)g.sender_off[k];
     ca.members = a.members;
     uint64_t off = 0;
+    const uint64_t per_word = cascade_scratch_words_per_word(g);
     for (uint32_t k = 1; k + 2 <= g.me; ++k) {
         ca.R[k] = scratch + off;
-        off += W * g.S[k];
+        if (job.check) ca.tag[k] = scratch + W * per_word + off;
+        off += W * casc_level_words((int)g.L, (int)k);
     }
+    ca.epoch = job.epoch & 0xffffffffull;
+    ca.inject = job.check == 2 ? 1u : 0u;
     ca.cnt = d_cnt;
     uint32_t coff = 0;
     for (uint32_t k = 0; k + 3 < g.me; ++k) {
@@ -461,23 +568,40 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
         coff += (uint32_t)(W * g.S[k]);
     }
     ca.cnt_off[g.me - 3] = coff;  // root counters
+    ca.h = job.h;
+    ca.ub = job.ub;
+    ca.votes = job.votes;
     ca.decisions = a.decisions ? a.decisions + trial0 : nullptr;
     ca.outcome = a.outcome ? a.outcome + trial0 : nullptr;
-    ca.counters = a.counters;
+    ca.counters = job.h ? nullptr : a.counters;
     ca.sk = a.sink;
     ProfScope ps(a.prof, "k_cascade", a.stream);
     if (const char* d = getenv("BA_CASC_DIAG")) {  // lab ablations, n=16 m=5 only
-        if (g.n == 16 && g.me == 5) switch (atoi(d)) {
-            case 2: return launch_cascade_t<16, 5, 2>(ca, a.cu_count, a.stream);
-            case 4: return launch_cascade_t<16, 5, 4>(ca, a.cu_count, a.stream);
+        if (g.n == 16 && g.me == 5 && job.h == 0 && !job.check) switch (atoi(d)) {
+            case 2: return launch_cascade_t<16, 5, 2>(ca, a.stream);
+            case 4: return launch_cascade_t<16, 5, 4>(ca, a.stream);
             default: break;
         }
     }
+    if (job.check) {
+#define BA_CASC_CHECK_LAUNCH(nn, mm) \
+    if (g.n == nn && g.me == mm) return launch_cascade_t<nn, mm, 0, true>(ca, a.stream);
+        BA_CASC_CHECK_SHAPES(BA_CASC_CHECK_LAUNCH)
+#undef BA_CASC_CHECK_LAUNCH
+        return hipErrorInvalidValue;
+    }
 #define BA_CASC_LAUNCH(nn, mm) \
-    if (g.n == nn && g.me == mm) return launch_cascade_t<nn, mm>(ca, a.cu_count, a.stream);
+    if (g.n == nn && g.me == mm) return launch_cascade_t<nn, mm>(ca, a.stream);
     BA_CASC_SHAPES(BA_CASC_LAUNCH)
 #undef BA_CASC_LAUNCH
     return hipErrorInvalidValue;
+}
+
+bool cascade_check_supported(const Geometry& g) {
+#define BA_CASC_OK(nn, mm) if (g.n == nn && g.me == mm) return true;
+    BA_CASC_CHECK_SHAPES(BA_CASC_OK)
+#undef BA_CASC_OK
+    return false;
 }
 
 }  // namespace ba

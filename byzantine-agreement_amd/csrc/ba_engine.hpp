@@ -153,11 +153,21 @@ hipError_t launch_epilogue_w(const RunArgs& a, const Geometry& g, uint64_t W,
 
 // LEVELS in one launch (ba_cascade.hip): leaf-up units plus an in-launch
 // fan-in cascade of the majority levels above them, roots and quorum
+struct CascJob {
+    uint32_t h = 0;               // 0: the whole tree; 1 / 2: votes of the h-hop subtrees [ub, ue)
+    uint32_t ub = 0, ue = 0;
+    uint64_t* votes = nullptr;    // range mode: [(u - ub)(L - h) + c][W] (ba.h, ba_split_votes_device)
+    uint32_t check = 0;           // tests: 1 = epoch tags checked, 2 = and one stale tag injected
+    uint64_t epoch = 0;           // check: this launch's tag
+};
 bool cascade_supported(const Geometry& g);
+bool cascade_check_supported(const Geometry& g);
+bool cascade_range_supported(const Geometry& g, uint32_t h);
 uint64_t cascade_counters_per_word(const Geometry& g);       // 128-B counters per trial word
-uint64_t cascade_scratch_words_per_word(const Geometry& g);  // R_1..R_{me-2} words per trial word
+uint64_t cascade_scratch_words_per_word(const Geometry& g);  // R_1..R_{me-2} words per trial word (x2 with check tags)
 hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_sender,
-                          uint64_t* scratch, uint32_t* d_cnt, uint64_t trial0, uint64_t ntrials);
+                          uint64_t* scratch, uint32_t* d_cnt, uint64_t trial0, uint64_t ntrials,
+                          const CascJob& job);
 
 hipError_t launch_table(const RunArgs& a, uint64_t* partials);
 hipError_t launch_gen_inputs(const RunArgs& a, uint32_t* faulty_out, uint8_t* order_out);

@@ -114,6 +114,10 @@ typedef struct ba_params {
 #define BA_C_BOUND_VIOL 9      /* in-bound trials violating IC1 or IC2               */
 #define BA_C_FAULTY_TOTAL 10   /* sum of f over trials                               */
 #define BA_C_ATTACK_DECISIONS 11 /* lieutenant decisions == attack                   */
+/* Slot 14 is test-only: hand-off tag mismatches counted by the LEVELS cascade's
+ * check build (environment BA_CASC_CHECK=1, read per call; 0 on a correct run).
+ * Slot 15 is the multi-GPU entries' error flag (always 0 in returned counters). */
+#define BA_C_CHECK_MISMATCH 14
 
 typedef struct ba_counters {
     uint64_t v[BA_NCOUNTERS];

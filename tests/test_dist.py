@@ -324,6 +324,44 @@ def test_second_hop_votes_match_oracle_gpu(engine, n, m, B, nr):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,m,level,units", [(16, 5, 1, (0, 7, 14)), (16, 5, 2, (0, 1, 13, 100, 209)),
+                                             (8, 5, 1, (0, 6)), (8, 5, 2, (0, 5, 41)),
+                                             (16, 4, 1, (0, 9))])
+def test_split_votes_single_units_through_cascade(engine, monkeypatch, n, m, level, units):
+    """The subtree split through k_cascade's range mode (ba_split_votes_device on a
+    cascade shape with h <= m_eff - 3): ranges of ONE h-hop subtree (the fewest
+    units per word, so a block's units span several words), two-subtree ranges, at
+    batch 1 and 130; rows equal the oracle's, equal the multi-launch pipeline's
+    (BA_NO_CASCADE=1), and the profile shows k_cascade ran."""
+    from ba_amd import lib as L
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    per = n - 1 - level
+    for B in (1, 130):
+        kw = dict(seed=17 + B, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1,
+                  order_mode=L.ORDER_RANDOM, first_trial=64 * 9)
+        p = L.make_params(n, m, **kw)
+        W = (B + 63) // 64
+        v_or = (oracle_c.votes if level == 1 else oracle_c.votes2)(n, m, B, **kw)
+        for ub in units:
+            for ue in (ub + 1, min(ub + 2, L.split_units(n, m, level))):
+                got = {}
+                for casc in ("1", "0"):
+                    monkeypatch.setenv("BA_NO_CASCADE", "0" if casc == "1" else "1")
+                    v = torch.zeros(((ue - ub) * per, W), dtype=torch.int64, device=dev)
+                    engine.profile(True)
+                    engine.split_votes_device(p, B, level, ub, ue, v.data_ptr(), stream=s)
+                    torch.cuda.synchronize()
+                    prof = engine.profile_read()
+                    engine.profile(False)
+                    assert ("k_cascade" in prof) == (casc == "1"), prof
+                    got[casc] = v.cpu().numpy().view(np.uint64)
+                assert np.array_equal(got["1"], oracle_c.pack_votes(v_or, ub, ue)), (B, ub, ue)
+                assert np.array_equal(got["1"], got["0"])
+    monkeypatch.delenv("BA_NO_CASCADE")
+
+
+@pytest.mark.gpu
 def test_split_multi_world1_equals_unsplit_n16_m5(engine):
     """Config 5 through ba_run_instance_split_multi on a one-rank RCCL communicator
     equals ba_run_trials on the same params, and equals the C port on the full
@@ -362,10 +400,11 @@ def force_split(monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("B", [1, 70])
 @pytest.mark.parametrize("level", [1, 2])
-def test_forced_split_world1_matches_oracle(engine, force_split, level):
-    """Config 5 (n=16, m=5), batch 70, through ba_run_instance_split_level_multi with
-    the split forced at world 1: decisions, outcome bytes and counters equal the
+def test_forced_split_world1_matches_oracle(engine, force_split, level, B):
+    """Config 5 (n=16, m=5), batch 1 and 70, through ba_run_instance_split_level_multi
+    with the split forced at world 1 (the votes through k_cascade's range mode): decisions, outcome bytes and counters equal the
     oracle (every rank's rows are its own, so the broadcast's layout -- rows
     [ub*row, ue*row) of rank 0 -- must be the one the root pass reads)."""
     from ba_amd import dist as D
@@ -374,7 +413,6 @@ def test_forced_split_world1_matches_oracle(engine, force_split, level):
     kw = dict(seed=0xBA5EED, faulty_mode=L.FAULTY_RANDOM, f=5, order_mode=L.ORDER_RANDOM,
               first_trial=64 * 7)
     p = L.make_params(16, 5, **kw)
-    B = 70
     comm = L.Comm(engine, 1, 0, L.comm_unique_id())
     try:
         for _ in range(2):  # the second call reuses the grown vote buffer

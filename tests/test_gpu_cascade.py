@@ -69,17 +69,82 @@ def test_cascade_chunks(monkeypatch):
 @pytest.mark.parametrize("n,m,B", [(16, 5, 1024), (16, 5, 1), (10, 3, 65536), (9, 4, 3000)])
 def test_cascade_equals_multi_launch_pipeline(engine, monkeypatch, n, m, B):
     """Config 5's full batch (and others): the one-launch cascade and the
-    multi-launch LEVELS pipeline give the same bits; repeated calls on one ctx
-    (counters reset by their last arrivers) too."""
+    multi-launch LEVELS pipeline give the same bits; a second cascade call on the
+    same ctx with DIFFERENT inputs (seed, first_trial) too -- a hand-off that read
+    the previous call's R words would show here, where identical inputs would hide
+    it -- with the fan-in counters reset by their last arrivers in between."""
     from ba_amd import lib as L
-    kw = dict(seed=0xBA5EED, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3, order_mode=L.ORDER_RANDOM)
-    a = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
-    a2 = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
+    kw1 = dict(seed=0xBA5EED, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3, order_mode=L.ORDER_RANDOM)
+    kw2 = dict(seed=0x5EED5, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3, order_mode=L.ORDER_RANDOM,
+               first_trial=64 * 1001)
+    a1 = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw1)
+    a2 = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw2)
     monkeypatch.setenv("BA_NO_CASCADE", "1")
-    b = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
+    b1 = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw1)
+    b2 = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw2)
     monkeypatch.delenv("BA_NO_CASCADE")
-    for r in (a2, b):
-        same(r.decisions, a.decisions, "decisions")
-        same(r.outcome, a.outcome, "outcome")
-        assert r.counters == a.counters
+    for a, b in ((a1, b1), (a2, b2)):
+        same(a.decisions, b.decisions, "decisions")
+        same(a.outcome, b.outcome, "outcome")
+        assert a.counters == b.counters
+    assert not np.array_equal(a1.decisions, a2.decisions)  # the inputs did change
 
+
+# --- hand-off check build (BA_CASC_CHECK, ba_cascade.hip CHECK) ---------------------
+def _check_calls(engine, n, m, batches, calls, mode):
+    """`calls` cascade calls on one ctx, batch sizes cycling through `batches`, each
+    with its own seed and first_trial (inputs drawn in-kernel), in the check build;
+    returns (mismatch count of every call, results of the calls kept for the oracle)."""
+    import torch
+    from ba_amd import lib as L
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    bmax = max(batches)
+    dec = torch.empty(bmax, dtype=torch.int64, device=dev)
+    out = torch.empty(bmax, dtype=torch.uint8, device=dev)
+    cnt = torch.zeros((calls, 16), dtype=torch.int64, device=dev)
+    kept = []
+    for i in range(calls):
+        B = batches[i % len(batches)]
+        kw = dict(seed=0xC0DE + 7919 * i, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + i % 2,
+                  order_mode=L.ORDER_RANDOM, first_trial=64 * (13 * i + 1))
+        engine.run_device(L.make_params(n, m, engine=L.ENGINE_LEVELS, **kw), B,
+                          d_decisions=dec.data_ptr(), d_outcome=out.data_ptr(),
+                          d_counters=cnt[i].data_ptr(), stream=s)
+        if i < 2 or i == calls - 1:
+            torch.cuda.synchronize()
+            kept.append((B, kw, dec[:B].cpu().numpy().view(np.uint64).copy(), out[:B].cpu().numpy().copy(),
+                         cnt[i].cpu().tolist()))
+    torch.cuda.synchronize()
+    c = cnt.cpu().numpy()
+    return c[:, 14], c, kept
+
+
+@pytest.mark.parametrize("n,m,batches,calls", [(16, 5, (1, 1024), 120), (8, 5, (1, 700, 64), 60),
+                                               (10, 3, (1, 4096), 60)])
+def test_cascade_handoff_tags(engine, monkeypatch, n, m, batches, calls):
+    """Every child word a cascade step reads carries this launch's epoch tag: over
+    >= 100 calls that alternate batch 1 and 1024 at n=16, m=5 (and other shapes),
+    with new inputs on every call, no step ever reads a word that a hand-off of
+    the same launch had not yet written (0 mismatches); the check build's results
+    are the oracle's."""
+    from ba_amd import lib as L
+    monkeypatch.setenv("BA_CASC_CHECK", "1")
+    mism, cnt, kept = _check_calls(engine, n, m, batches, calls, 1)
+    assert int(mism.sum()) == 0, f"stale hand-off reads: {mism.nonzero()}"
+    assert (cnt[:, 0] > 0).all()
+    for B, kw, d, o, c in kept:
+        od, oo, oc = (oracle_c.sliced_run if B > 64 else oracle_c.run)(n, m, B, **kw)
+        same(d, od, "decisions")
+        same(o, oo, "outcome")
+        assert c[:len(L.COUNTER_NAMES)] == list(oc.values())
+
+
+@pytest.mark.parametrize("n,m", [(16, 5), (8, 5), (10, 3)])
+def test_cascade_handoff_detector_fires(engine, monkeypatch, n, m):
+    """BA_CASC_CHECK=2: the launch's first unit stores a stale tag beside its R word;
+    the step that reads it must count exactly one mismatch per launch (the
+    detector of test_cascade_handoff_tags can see a stale read)."""
+    monkeypatch.setenv("BA_CASC_CHECK", "2")
+    mism, _, _ = _check_calls(engine, n, m, (1, 130), 6, 2)
+    assert mism.tolist() == [1] * 6

@@ -192,8 +192,11 @@ def test_header_constants_agree():
              "BA_ENGINE_FUSED": L.ENGINE_FUSED, "BA_ENGINE_LEVELS": L.ENGINE_LEVELS}
     for k, v in pairs.items():
         assert int(defs[k]) == v, k
-    names = re.findall(r"#define BA_C_\w+ (\d+)", hdr)
-    assert [int(x) for x in names] == list(range(len(L.COUNTER_NAMES)))
+    names = re.findall(r"#define BA_C_(\w+) (\d+)", hdr)
+    run = [int(x) for k, x in names if k != "CHECK_MISMATCH"]
+    assert run == list(range(len(L.COUNTER_NAMES)))
+    # the test-only hand-off check slot sits past the run counters, below the error flag
+    assert dict(names)["CHECK_MISMATCH"] == str(L.NCOUNTERS - 2)
     assert L.COUNTER_NAMES == O.COUNTERS == oracle_c.COUNTER_NAMES
 
 
