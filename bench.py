@@ -174,17 +174,19 @@ def cpu_threads() -> int:
         return os.cpu_count() or 1
 
 
-def run_cpu_baseline(n, m, seed, fmax, budget_s, first, count, gpu_counters):
+def run_cpu_baseline(n, m, seed, fmax, budget_s, ranges, gpu_counters, extra_first):
     """Time the word-sliced OpenMP C port (oracle/ba_sliced.c: 64 trials per word,
     one Philox call per two slot-words, the GPU engines' minimum draw count) on a
     bounded sample of the same workload, inputs staged first as on the GPU.
 
-    The sample starts with exactly the trials of the GPU's timed steps,
-    [first, first + count): the port's run counters over them must equal the
-    GPU's (the quorum / IC tallies of ba.py:197-255), else the
-    bench exits non-zero.  It then continues with the next trials of the same
-    stream until ~budget_s of CPU work; `value` is all sampled trials over the
-    time of both runs."""
+    The sample starts with exactly the trials this rank's GPU resolved in its
+    timed steps, `ranges` = [(first, count), ...] (one contiguous range at world
+    1; one range per step at world N, trials shard by step): the port's run
+    counters over them must equal this rank's GPU counters from before the
+    all-reduce (the quorum / IC tallies of ba.py:197-255), else the
+    bench exits non-zero.  It then continues with trials from `extra_first` on
+    (outside every rank's timed ranges) until ~budget_s of CPU work; `value` is
+    all sampled trials over the time of both runs."""
     import oracle_c
     threads = cpu_threads()
     kw = dict(seed=seed, faulty_mode=1, f=fmax, order_mode=1)
@@ -196,37 +198,79 @@ def run_cpu_baseline(n, m, seed, fmax, budget_s, first, count, gpu_counters):
                                       threads=threads, want_outputs=False)
         return c, time.perf_counter() - t0
 
-    c_gpu_range, dt0 = timed_run(first, count)
-    want = {k: gpu_counters[k] for k in c_gpu_range}
-    match = c_gpu_range == want
+    got, dt0, count = None, 0.0, 0
+    for f0, cnt in ranges:
+        c, dt = timed_run(f0, cnt)
+        got = c if got is None else {k: got[k] + c[k] for k in got}
+        dt0 += dt
+        count += cnt
+    want = {k: gpu_counters[k] for k in got}
+    match = got == want
     if not match:
-        raise SystemExit(f"cpu_baseline: the C port's counters over the GPU's timed trials "
-                         f"[{first}, {first + count}) differ from the GPU's: {c_gpu_range} vs {want}")
+        raise SystemExit(f"cpu_baseline: the C port's counters over this GPU's timed trials "
+                         f"({len(ranges)} ranges, {count} trials) differ from the GPU's: {got} vs {want}")
     rate = count / max(dt0, 1e-9)
     extra = int(min(max(rate * budget_s - count, 0), 1 << 27)) // 64 * 64
     dt1 = 0.0
     if extra:
-        _, dt1 = timed_run(first + count, extra)
+        _, dt1 = timed_run(extra_first, extra)
     sample, dt = count + extra, dt0 + dt1
     value = sample / dt
     nproc = os.cpu_count() or 1
+    where = (f"trials [{ranges[0][0]}, {ranges[0][0] + count})" if len(ranges) == 1 else
+             f"this rank's {len(ranges)} step ranges of {ranges[0][1]} trials (first {ranges[0][0]})")
     return {"value": round(value, 1), "unit": "trial-decisions/s", "cores": threads, "kind": "port",
             "sample": f"word-sliced OpenMP C port (oracle/ba_sliced.c, x{threads} threads) on "
-                      f"trials [{first}, {first + sample}) of the same n={n}, m={m} synthetic "
-                      f"stream: the GPU's {count} timed trials, then {extra} more (inputs "
-                      f"staged first, as on the GPU), {dt:.1f} s; host CPU: {cpu_model()}, "
-                      f"nproc={nproc}; {threads} threads = this job's CPU share "
-                      f"(OMP_NUM_THREADS / affinity)",
+                      f"{where} of the same n={n}, m={m} synthetic stream: this GPU's {count} timed "
+                      f"trials, then {extra} more from trial {extra_first} (inputs staged first, as "
+                      f"on the GPU), {dt:.1f} s; host CPU: {cpu_model()}, nproc={nproc}; {threads} "
+                      f"threads = this job's CPU share (OMP_NUM_THREADS / affinity)",
             "per_thread_value": round(value / threads, 1),
             "all_cores_projection": {"value": round(value / threads * nproc, 1), "cores": nproc,
                                      "note": "per-thread rate x nproc, not measured (the pool "
                                              "grants this job its CPU share only)"},
             "counters_match": match,
-            "counters_checked": {"first_trial": first, "trials": count,
-                                 "what": "all 12 run counters of the GPU's timed steps"},
+            "counters_checked": {"ranges": len(ranges), "first_trial": ranges[0][0], "trials": count,
+                                 "what": "all 12 run counters of this rank's timed steps (before "
+                                         "the all-reduce)"},
             "reference_ba_py": {"value_us_per_trial": 574.0, "config": "OM(1) n=10, one core",
                                 "where": "dev container (Intel Xeon), BASELINE.md; ba.py cannot "
                                          "run on the GPU box (rpyc and the reference are absent)"}}
+
+
+def clock_from_probes(p0, p1):
+    """Average engine clock between two ba_clock_probe_device probes, per XCD:
+    (d s_memtime / d s_memrealtime) x 100 MHz, rows {xcc, hw, memtime, realtime}
+    (the median row of each XCD in each probe).  Returns (median MHz, {xcc: MHz})."""
+    import statistics
+
+    def per_xcc(rows):
+        d = {}
+        for xcc, _, mt, rt in rows:
+            d.setdefault(int(xcc), []).append((int(mt), int(rt)))
+        return {k: sorted(v)[len(v) // 2] for k, v in d.items()}
+    a, b = per_xcc(p0), per_xcc(p1)
+    mhz = {}
+    for k in sorted(set(a) & set(b)):
+        dmt, drt = b[k][0] - a[k][0], b[k][1] - a[k][1]
+        if drt > 0 and dmt > 0:
+            mhz[k] = round(dmt / drt * 100.0, 1)
+    return (statistics.median(mhz.values()) if mhz else None), mhz
+
+
+def first_trial(i: int, rank: int, world: int, batch: int) -> int:
+    """Global index of the first trial of step slot i on `rank`: slot i of the
+    job is world x batch consecutive trials, rank r's shard the r-th batch of
+    them (weak scaling, disjoint shards; Philox keyed by global trial index)."""
+    return (i * world + rank) * batch
+
+
+def rank_ranges(base: int, steps: int, rank: int, world: int, batch: int) -> list:
+    """The (first, count) trial ranges one rank resolves in the timed steps
+    base .. base+steps-1: one contiguous range at world 1, one per step otherwise."""
+    if world == 1:
+        return [(first_trial(base, 0, 1, batch), batch * steps)]
+    return [(first_trial(base + i, rank, world, batch), batch) for i in range(steps)]
 
 
 def free_port() -> int:
@@ -347,7 +391,7 @@ def main():
     outs = [torch.empty(B, dtype=torch.uint8, device=dev) for _ in range(NS)]
 
     def first_of(i):
-        return (i * world + rank) * B  # global trial index: weak scaling, disjoint shards
+        return first_trial(i, rank, world, B)
 
     # every step's inputs staged in HBM and every step's params built before timing
     n_warm_slots = args.warmup + 2
@@ -400,8 +444,10 @@ def main():
     warm_s = time.perf_counter() - t_w
 
     bar = torch.zeros(16, dtype=torch.int64, device=dev)  # RCCL barrier operand
+    local_cnt = torch.zeros(16, dtype=torch.int64, device=dev)  # this rank's counters, pre all-reduce
+    probes = torch.zeros((2, L.PROBE_BLOCKS, 4), dtype=torch.int64, device=dev)
 
-    def timed(base, in_kernel, ns=NS):
+    def timed(base, in_kernel, ns=NS, probe=False):
         cnt.zero_()
         torch.cuda.synchronize(dev)
         if dist:
@@ -412,6 +458,8 @@ def main():
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
+        if probe:  # the clock pass (untimed): one probe before the steps, one after
+            eng.clock_probe_device(probes[0].data_ptr(), stream=sp)
         ev0.record(stream)
         for j in range(1, ns):
             streams[j].wait_event(ev0)
@@ -420,16 +468,22 @@ def main():
         for j in range(1, ns):
             stream.wait_stream(streams[j])
         ev1.record(stream)
+        if probe:
+            eng.clock_probe_device(probes[1].data_ptr(), stream=sp)
         if comm is not None:
+            local_cnt.copy_(cnt)  # 128 B on the stream: the rank's own tallies (cpu_baseline)
             # the only collective: the run counters (RCCL).  It is also the closing
             # barrier: it completes on a rank only after every rank's steps ended.
             comm.allreduce_device(cptr, stream=sp)
         torch.cuda.synchronize(dev)
         if dist and comm is None:  # gloo fallback: host all-reduce, then a host barrier
             host = cnt.cpu()
+            local_cnt.copy_(host)
             dist.all_reduce(host)
             cnt.copy_(host)
             dist.barrier()
+        if not dist:
+            local_cnt.copy_(cnt)
         wall = time.perf_counter() - t0
         elapsed = torch.tensor([wall], dtype=torch.float64)
         if dist:
@@ -440,6 +494,7 @@ def main():
     base = n_warm_slots
     T, gpu_ms = timed(base, args.inputs_in_kernel)
     counters = dict(zip(L.COUNTER_NAMES, [int(x) for x in cnt.cpu().tolist()]))
+    local_counters = dict(zip(L.COUNTER_NAMES, [int(x) for x in local_cnt.cpu().tolist()]))
     value = total_trials / T
     value_gen = gen_ms = None
     if not args.inputs_in_kernel:
@@ -455,6 +510,12 @@ def main():
     if counters1 != counters:
         raise SystemExit(f"{NS}-stream and one-stream runs disagree: {counters} vs {counters1}")
     value_1 = total_trials / T1
+    # the clock pass: the timed region's steps again (untimed), bracketed by two
+    # engine-clock probes on the launch stream (attributes a run's
+    # rate to the clock it ran at)
+    Tc, gpu_ms_c = timed(base, args.inputs_in_kernel, NS, probe=True)
+    pr = probes.cpu().numpy()
+    sclk, sclk_xcd = clock_from_probes(pr[0], pr[1])
 
     # per-kernel HIP-event timing on the launch stream (a further pass of new steps)
     kernels, roof, valu_roof, compute_roof, side = {}, None, None, None, None
@@ -550,10 +611,12 @@ def main():
                         "once and read once): moved by the LEVELS engine, NOT by this kernel; a "
                         "comparison figure only"}
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        # the GPU's timed steps at world 1: trials [base*B, (base+K)*B), contiguous
-        cpu = run_cpu_baseline(n, m, args.seed, fmax, args.cpu_budget_s, first_of(base),
-                               B * args.steps, counters)
+    if rank == 0 and not args.no_cpu:
+        # this rank's timed steps: trials [first_of(i), first_of(i) + B) for i in the
+        # timed slots (contiguous at world 1); checked against its pre-all-reduce counters
+        cpu = run_cpu_baseline(n, m, args.seed, fmax, args.cpu_budget_s,
+                               rank_ranges(base, args.steps, rank, world, B), local_counters,
+                               first_trial(n_total, 0, world, B))
 
     if rank == 0:
         line = {
@@ -580,6 +643,14 @@ def main():
             "value_with_input_generation": round(value_gen, 1) if value_gen else None,
             "ms_per_step_with_input_generation_gpu_events": round(gen_ms / args.steps, 4) if gen_ms else None,
             "warm_up_s": round(warm_s, 2),
+            "sclk_mhz_timed": sclk,
+            "clock": {"sclk_mhz_median_xcd": sclk, "per_xcd_mhz": {str(k): v for k, v in sclk_xcd.items()},
+                      "ms_per_step_gpu_events_clock_pass": round(gpu_ms_c / args.steps, 4),
+                      "value_at_2400mhz": round(value * 2400.0 / sclk, 1) if sclk else None,
+                      "note": "engine clock over a replica of the timed region (same steps, streams "
+                              "and schedule, untimed), from two s_memtime/s_memrealtime probes "
+                              "bracketing it (ba_clock_probe_device); value_at_2400mhz = value x "
+                              "2400 / sclk: a labelled side figure, not a measurement"},
             "kernels_ms": {k: round(v[1] / v[0], 4) for k, v in kernels.items()},
             "roofline": roof,
             "valu_roofline": valu_roof,

@@ -42,7 +42,9 @@ EXPORTS = ["ba_version", "ba_device_count", "ba_ctx_create", "ba_ctx_destroy", "
            "ba_comm_allreduce_device", "ba_comm_allgather_votes_device",
            "ba_run_instance_split_multi", "ba_split_units", "ba_split_vote_slots",
            "ba_split_share", "ba_split_votes_device", "ba_root_from_split_votes_device",
-           "ba_comm_allgather_split_votes_device", "ba_run_instance_split_level_multi"]
+           "ba_comm_allgather_split_votes_device", "ba_run_instance_split_level_multi",
+           "ba_clock_probe_device"]
+PROBE_BLOCKS = 64  # BA_PROBE_BLOCKS
 
 
 class BAError(RuntimeError):
@@ -127,6 +129,7 @@ def load(path: str | None = None):
                                               vp, vp]
     lib.ba_ctx_device.argtypes = [vp, ctypes.POINTER(i32)]
     lib.ba_ctx_stream.argtypes = [vp, ctypes.POINTER(vp)]
+    lib.ba_clock_probe_device.argtypes = [vp, vp, vp]
     lib.ba_comm_unique_id.argtypes = [ctypes.c_char_p]
     lib.ba_comm_create.argtypes = [vp, i32, i32, ctypes.c_char_p, ctypes.POINTER(vp)]
     lib.ba_comm_destroy.argtypes = [vp]
@@ -291,6 +294,11 @@ class Engine:
         _check(self.lib, self.lib.ba_subtree_votes_device(
             self.handle, ctypes.byref(params), batch, j_begin, j_end, d_faulty or None,
             d_order or None, d_votes, stream or None))
+
+    def clock_probe_device(self, d_out: int, stream=0):
+        """Enqueue the engine-clock probe (ba_clock_probe_device): PROBE_BLOCKS rows of
+        {XCC id, HW id, s_memtime, s_memrealtime} into d_out (uint64)."""
+        _check(self.lib, self.lib.ba_clock_probe_device(self.handle, d_out, stream or None))
 
     def split_votes_device(self, params: Params, batch: int, level: int, u_begin: int, u_end: int,
                            d_votes: int, d_faulty=0, d_order=0, stream=0):

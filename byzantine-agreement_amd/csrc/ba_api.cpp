@@ -382,6 +382,17 @@ extern "C" int ba_ctx_device(ba_ctx* ctx, int* device) {
     return BA_OK;
 }
 
+namespace ba {
+hipError_t launch_clock_probe(uint64_t* d_out, uint32_t blocks, hipStream_t st);  // ba_probe.hip
+}
+
+extern "C" int ba_clock_probe_device(ba_ctx* ctx, uint64_t* d_out, void* stream) {
+    if (!ctx || !d_out) return fail(BA_EINVAL, "ctx and d_out are required");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(ba::launch_clock_probe(d_out, BA_PROBE_BLOCKS, stream ? (hipStream_t)stream : ctx->stream));
+    return BA_OK;
+}
+
 extern "C" int ba_ctx_stream(ba_ctx* ctx, void** stream) {
     if (!ctx || !stream) return fail(BA_EINVAL, "ctx and stream are required");
     *stream = (void*)ctx->stream;

@@ -338,6 +338,16 @@ int ba_profile_enable(struct ba_ctx* ctx, int on);
 int ba_profile_read(struct ba_ctx* ctx, int index, char* name, int name_len,
                     uint64_t* launches, double* total_ms);
 
+/* Engine-clock probe (measurement aux; no ba.py analogue).  Enqueues on `stream`
+ * one tiny launch of BA_PROBE_BLOCKS one-wave blocks; block b writes
+ * d_out[4b .. 4b+3] = {XCC id, HW id, s_memtime, s_memrealtime}.  s_memtime
+ * counts shader-clock cycles, s_memrealtime a constant 100 MHz clock, so two
+ * probes bracketing a stretch of work give that stretch's average engine clock
+ * per XCD: (dmemtime / drealtime) x 100 MHz (MI355X_MICROARCH.md).  bench.py
+ * brackets a replica of its timed region with two probes. */
+#define BA_PROBE_BLOCKS 64
+int ba_clock_probe_device(struct ba_ctx* ctx, uint64_t* d_out, void* stream);
+
 /* ---- ba.py's coin source (host only, no device needed) --------------------
  * Replaces the unseeded global CPython MT19937 behind random.randint(0, 1)
  * (ba.py:45 relay lies, ba.py:269 commander lies).  ba_mt_seed(s) equals

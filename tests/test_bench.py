@@ -103,9 +103,76 @@ def test_cpu_baseline_checks_counters_against_gpu():
     n, m, first, count = 10, 3, 64 * 1000, 64 * 50
     _, _, want = oracle_c.run(n, m, count, seed=5, faulty_mode=1, f=3, order_mode=1,
                               first_trial=first)
-    cpu = bench.run_cpu_baseline(n, m, 5, 3, 0.0, first, count, dict(want))
+    cpu = bench.run_cpu_baseline(n, m, 5, 3, 0.0, [(first, count)], dict(want), 64 * 5000)
     assert cpu["counters_match"] is True and cpu["counters_checked"]["trials"] == count
     assert cpu["value"] > 0 and cpu["kind"] == "port"
     bad = dict(want, agreement=want["agreement"] + 1)
     with pytest.raises(SystemExit):
-        bench.run_cpu_baseline(n, m, 5, 3, 0.0, first, count, bad)
+        bench.run_cpu_baseline(n, m, 5, 3, 0.0, [(first, count)], bad, 64 * 5000)
+
+
+def test_rank_ranges_shard_the_timed_trials():
+    """Every rank's timed ranges are disjoint, B trials per step, and together
+    cover exactly the job's timed slots."""
+    B, base, K = 128, 5, 4
+    assert bench.rank_ranges(base, K, 0, 1, B) == [(base * B, K * B)]
+    for world in (2, 3, 8):
+        seen = set()
+        for r in range(world):
+            rr = bench.rank_ranges(base, K, r, world, B)
+            assert len(rr) == K and all(c == B for _, c in rr)
+            for f0, c in rr:
+                seen.update(range(f0, f0 + c))
+        assert seen == set(range(base * world * B, (base + K) * world * B))
+
+
+def _cpu_baseline_rank(rank, world, port, q):
+    """One gloo rank of the N>1 bench flow with the C oracle as the GPU stand-in:
+    its local counters over rank_ranges, the all-reduce, then rank 0's CPU leg
+    checked against its PRE-all-reduce counters (the job's totals must fail it)."""
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_c
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        import torch
+        n, m, B, base, K, seed, fmax = 10, 3, 192, 3, 3, 0x77, 3
+        local = None
+        for f0, c in bench.rank_ranges(base, K, rank, world, B):
+            _, _, cc = oracle_c.run(n, m, c, seed=seed, faulty_mode=1, f=fmax, order_mode=1,
+                                    first_trial=f0)
+            local = cc if local is None else {k: local[k] + cc[k] for k in local}
+        t = torch.tensor(list(local.values()), dtype=torch.int64)
+        dist.all_reduce(t)
+        total = dict(zip(local, t.tolist()))
+        if rank == 0:
+            cpu = bench.run_cpu_baseline(n, m, seed, fmax, 0.0, bench.rank_ranges(base, K, 0, world, B),
+                                         local, bench.first_trial(base + K + 2, 0, world, B))
+            ok = cpu["counters_match"] and cpu["counters_checked"]["ranges"] == K
+            try:
+                bench.run_cpu_baseline(n, m, seed, fmax, 0.0, bench.rank_ranges(base, K, 0, world, B),
+                                       total, 0)
+                ok = False
+            except SystemExit:
+                pass
+            q.put(ok and total["trials"] == world * K * B)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cpu_baseline_world2_gloo():
+    """bench.py's N>1 CPU leg: rank 0 checks the port against its own timed ranges
+    with its pre-all-reduce counters (world 2, gloo, CPU)."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = bench.free_port()
+    ps = [ctx.Process(target=_cpu_baseline_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in ps)
+    assert q.get(timeout=5) is True
