@@ -52,6 +52,27 @@ for s in $STAGES; do
          python3 tools/pmc_summary.py gpurun_out/pmc gpurun_out/pmc_summary.json \
            --workload "bench.py default: n=10 m=3, 1048576 trials/step" --config 10,3,1048576,auto,k_om3w > gpurun_out/pmc_summary.log 2>&1 ;;
     configs) run configs 600 python -u tools/run_configs.py || exit $? ;;
+    c5) run c5_1024 300 python -u tools/config5_prof.py --batch 1024 --split || exit $?
+        run c5_1 300 python -u tools/config5_prof.py --batch 1 --reps 500 --split || exit $? ;;
+    c5ab) for r in 1 2; do for lib in byzantine-agreement_amd/ba_amd/libba_hip.so ab/libba_noacq.so; do
+            t=$(basename $lib .so)_$r
+            run c5ab_1024_$t 300 env BA_HIP_LIB=$ROOT/$lib python -u tools/config5_prof.py --batch 1024 || exit $?
+            run c5ab_1_$t 300 env BA_HIP_LIB=$ROOT/$lib python -u tools/config5_prof.py --batch 1 --reps 500 || exit $?
+          done; done ;;
+    c5prof) for b in 1024 1; do
+          (cd /tmp && export TMPDIR=/tmp && mkdir -p "$ROOT/gpurun_out/c5prof_$b" && \
+           timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/c5prof_$b" -o run -- \
+             python3 "$ROOT/tools/config5_prof.py" --batch $b --reps 300 > "$ROOT/gpurun_out/c5prof_$b.log" 2>&1); rc=$?
+          echo "c5prof $b rc=$rc" | tee -a gpurun_out/steps.log; [ $rc -eq 0 ] || exit $rc; done ;;
+    c5pmc) C5="$ROOT/tools/config5_prof.py --batch 1024 --reps 50"
+         for pass in "sq:SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
+                     "lds:SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
+                     "fetch:FETCH_SIZE GRBM_GUI_ACTIVE GRBM_COUNT" "write:WRITE_SIZE"; do
+           name=${pass%%:*}; ctrs=${pass#*:}
+           (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --pmc $ctrs --output-format csv \
+              -d "$ROOT/gpurun_out/c5pmc" -o "$name" -- python3 $C5 > "$ROOT/gpurun_out/c5pmc_$name.log" 2>&1)
+           rc=$?; echo "c5pmc $name rc=$rc" | tee -a gpurun_out/steps.log; [ $rc -eq 0 ] || exit $rc
+         done ;;
     *) echo "unknown stage $s"; exit 2 ;;
   esac
 done
