@@ -45,9 +45,19 @@ __host__ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32
 __host__ __device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) { return maj3_32(a, b, c); }
 
 // ---------------------------------------------------------------------------
-// Philox4x32-10 (Salmon et al., SC'11).  The key is kernel-uniform, so the key
-// schedule lives in SGPRs; each round is 2 x v_mad_u64_u32 + 2 x xor3
-// (tools/philox_bench: 9.5e11 calls/s on one MI355X vs 7.8e11 with 2-input xors).
+// Philox4x32-10 (Salmon et al., SC'11).  Each round is 2 x v_mad_u64_u32 +
+// 2 x xor3 (tools/philox_bench: 9.5e11 calls/s on one MI355X vs 7.8e11 with
+// 2-input xors).  The key is kernel-uniform; where its round keys live is a
+// build choice of philox10_n (same results on every path):
+//   default           groups of 2-4 calls: round keys as VGPR operands (KeysV,
+//                     philox10_n_vk; a VALU op with an SGPR operand issues
+//                     slower), rounds 2-9 as one generated asm
+//                     statement (ba_philox_asm.hpp)
+//   BA_PHILOX_SKEYS   groups of 2-4 calls: round keys in SGPRs, rounds 0-1 in
+//                     C, rounds 2-9 as the asm statement
+//   G = 1 (and any    the generic round loop, keys in SGPRs, products pinned
+//   BA_PHILOX_C /     to v_mad_u64_u32 from round 2 (BA_PHILOX_C: plain C
+//   BA_PHILOX_ROUND_ASM build)  products; both switches are A/B builds only)
 // ---------------------------------------------------------------------------
 struct P4 {
     uint32_t x, y, z, w;

@@ -296,28 +296,42 @@ static bool force_split() {
 }
 
 // Sum every rank's error flag now, synchronously, before a collective that a
-// failed rank could not join.  Returns BA_OK when no rank failed; otherwise
-// this rank's own error, or "another rank failed" -- the same answer on every
-// rank, so all of them leave the call together.  The error slot is left at 0
-// for finish_job when no rank failed.
-static int preagree(ba_comm* comm, int local_rc) {
-    const uint64_t flag = local_rc != BA_OK ? 1 : 0;
+// failed rank could not join.  Returns BA_OK when this rank is to join the
+// exchange; otherwise this rank's own error, or "another rank failed" -- the
+// same answer on every rank, so all of them leave the call together.  The
+// error slot is left at 0 for finish_job when no rank failed.
+// This rank's own agreement transport can fail while its local work is valid:
+//  - flag upload: the flag is raised with a device memset instead (a failed
+//    upload counts as a failure every rank sees), so all ranks leave together;
+//  - read-back: its peers read the sum and, if no rank failed, enter the
+//    exchange, so this rank joins them too and reports the error after the
+//    exchange (*late) instead of leaving them waiting in the broadcasts.
+static int preagree(ba_comm* comm, int local_rc, int* late) {
+    uint64_t flag = local_rc != BA_OK ? 1 : 0;
     uint64_t got = 0;
-    int rc = BA_OK;
     Rccl& r = rccl();
+    int up = BA_OK;
     if (hipMemcpyAsync(comm->d_cnt + kErrSlot, &flag, sizeof flag, hipMemcpyHostToDevice,
-                       comm->stream) != hipSuccess)
-        rc = failf(BA_EDEVICE, "error-flag upload");
+                       comm->stream) != hipSuccess) {
+        up = failf(BA_EDEVICE, "error-flag upload");
+        flag = 1;  // raise it on the device: lowest byte 1 = a flag of 1
+        (void)hipMemsetAsync(comm->d_cnt + kErrSlot, 0, sizeof flag, comm->stream);
+        (void)hipMemsetAsync(comm->d_cnt + kErrSlot, 1, 1, comm->stream);
+    }
     const ncclResult_t e = r.all_reduce(comm->d_cnt + kErrSlot, comm->d_cnt + kErrSlot, 1, ncclUint64,
                                         ncclSum, comm->comm, comm->stream);
-    if (e != ncclSuccess && rc == BA_OK) rc = failf(BA_EDEVICE, "ncclAllReduce: %s", r.error_string(e));
-    if ((hipMemcpyAsync(&got, comm->d_cnt + kErrSlot, sizeof got, hipMemcpyDeviceToHost,
-                        comm->stream) != hipSuccess ||
-         hipStreamSynchronize(comm->stream) != hipSuccess) &&
-        rc == BA_OK)
-        rc = failf(BA_EDEVICE, "error-flag read-back");
+    if (e != ncclSuccess)  // the communicator itself failed: no exchange can follow
+        return local_rc != BA_OK ? local_rc : failf(BA_EDEVICE, "ncclAllReduce: %s", r.error_string(e));
+    if (hipMemcpyAsync(&got, comm->d_cnt + kErrSlot, sizeof got, hipMemcpyDeviceToHost,
+                       comm->stream) != hipSuccess ||
+        hipStreamSynchronize(comm->stream) != hipSuccess) {
+        if (local_rc != BA_OK || up != BA_OK) return local_rc != BA_OK ? local_rc : up;
+        *late = failf(BA_EDEVICE, "error-flag read-back");
+        (void)hipMemsetAsync(comm->d_cnt + kErrSlot, 0, sizeof got, comm->stream);
+        return BA_OK;
+    }
     if (local_rc != BA_OK) return local_rc;
-    if (rc != BA_OK) return rc;
+    if (up != BA_OK) return up;
     if (got != 0)
         return failf(BA_EDEVICE, "%llu other rank(s) failed this call before the vote exchange",
                      (unsigned long long)got);
@@ -401,8 +415,9 @@ extern "C" int ba_run_instance_split_level_multi(struct ba_ctx* ctx, struct ba_c
     // allocate its vote buffer cannot join the grouped broadcasts (its peers
     // would wait in them forever), so every rank learns of any failure here
     // and all of them skip the exchange together.
+    int late = BA_OK;  // this rank's agreement read-back failed: join the exchange, report after
     {
-        const int rc_pre = preagree(comm, local);
+        const int rc_pre = preagree(comm, local, &late);
         if (rc_pre != BA_OK) return rc_pre;
     }
     if (local == BA_OK && batch > 0) {
@@ -423,6 +438,7 @@ extern "C" int ba_run_instance_split_level_multi(struct ba_ctx* ctx, struct ba_c
         local = ba_root_from_split_votes_device(ctx, p, batch, level, d_faulty_mask, d_order,
                                                 comm->d_votes, d_decisions, d_outcome, comm->d_cnt,
                                                 comm->stream);
+    if (local == BA_OK) local = late;
     return finish_job(comm, local, counters_out, false);
 }
 
