@@ -447,6 +447,8 @@ def main():
     local_cnt = torch.zeros(16, dtype=torch.int64, device=dev)  # this rank's counters, pre all-reduce
     probes = torch.zeros((2, L.PROBE_BLOCKS, 4), dtype=torch.int64, device=dev)
 
+    host_enq = [0.0]  # ms from t0 until every step was enqueued (the last timed pass)
+
     def timed(base, in_kernel, ns=NS, probe=False):
         cnt.zero_()
         torch.cuda.synchronize(dev)
@@ -475,6 +477,13 @@ def main():
             # the only collective: the run counters (RCCL).  It is also the closing
             # barrier: it completes on a rank only after every rank's steps ended.
             comm.allreduce_device(cptr, stream=sp)
+        t_enq = time.perf_counter()
+        # close: poll the stream's last event until it has run (a blocking synchronize
+        # sleeps and wakes tens of us late), then synchronize
+        evz = torch.cuda.Event()
+        evz.record(stream)
+        while not evz.query():
+            pass
         torch.cuda.synchronize(dev)
         if dist and comm is None:  # gloo fallback: host all-reduce, then a host barrier
             host = cnt.cpu()
@@ -485,6 +494,7 @@ def main():
         if not dist:
             local_cnt.copy_(cnt)
         wall = time.perf_counter() - t0
+        host_enq[0] = (t_enq - t0) * 1e3
         elapsed = torch.tensor([wall], dtype=torch.float64)
         if dist:
             dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
@@ -493,6 +503,7 @@ def main():
     total_trials = B * args.steps * world
     base = n_warm_slots
     T, gpu_ms = timed(base, args.inputs_in_kernel)
+    enq_ms = host_enq[0]
     counters = dict(zip(L.COUNTER_NAMES, [int(x) for x in cnt.cpu().tolist()]))
     local_counters = dict(zip(L.COUNTER_NAMES, [int(x) for x in local_cnt.cpu().tolist()]))
     value = total_trials / T
@@ -636,6 +647,7 @@ def main():
                          "1M-trial pass with its own outputs; every step's counters summed and checked"
                          if NS > 1 else "one step at a time on one stream"),
             "ms_per_step_gpu_events": round(gpu_ms / args.steps, 4),
+            "host_enqueue_ms_per_step": round(enq_ms / args.steps, 4),
             "value_gpu_events": round(B * args.steps / (gpu_ms * 1e-3), 1),
             "streams": NS,
             "value_single_stream": round(value_1, 1),

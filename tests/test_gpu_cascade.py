@@ -87,7 +87,8 @@ def test_cascade_equals_multi_launch_pipeline(engine, monkeypatch, n, m, B):
         same(a.decisions, b.decisions, "decisions")
         same(a.outcome, b.outcome, "outcome")
         assert a.counters == b.counters
-    assert not np.array_equal(a1.decisions, a2.decisions)  # the inputs did change
+    if B >= 64:
+        assert not np.array_equal(a1.decisions, a2.decisions)  # the inputs did change
 
 
 # --- hand-off check build (BA_CASC_CHECK, ba_cascade.hip CHECK) ---------------------
