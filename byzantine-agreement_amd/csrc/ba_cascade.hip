@@ -294,13 +294,10 @@ __device__ __forceinline__ void casc_put(const CascArgs& a, uint32_t w, uint32_t
 // whole wave, lane r = receiver index among the K = L - q lieutenants not in
 // sigma.  in: the word's input planes (LDS); scr: the wave's LDS scratch.
 // mm: CHECK builds' per-lane count of child tags that were not this launch's.
-// LK: sigma's children are in LDS, kids[j*(K-1) + c] (the sigma-blocked kernel's
-// in-block step), not handed off through R_{q+1}.
-template <int N, int ME, int q, bool CHECK, bool LK = false>
+template <int N, int ME, int q, bool CHECK>
 __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in, uint64_t* scr,
                                           uint32_t lane, uint32_t w, uint32_t s, uint64_t gw,
-                                          TrialCounts& tc, uint32_t& mm,
-                                          const uint64_t* kids = nullptr) {
+                                          TrialCounts& tc, uint32_t& mm) {
     using C = Casc<N, ME>;
     constexpr int L = C::L, K = L - q;
     const bool act = lane < (uint32_t)K;
@@ -314,15 +311,11 @@ __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in,
     uint64_t cv[K - 1];
     static_for<0, K - 1>([&](auto jj) {
         const uint32_t j = (uint32_t)jj() + ((uint32_t)jj() >= r ? 1u : 0u);
-        const uint32_t c = j * (uint32_t)(K - 1) + r - (r > j ? 1u : 0u);
-        if constexpr (LK) {
-            cv[jj()] = act ? kids[c] : 0ull;
-        } else {
-            const uint64_t i = C::template addr<q + 1>(w, s * (uint32_t)(K * (K - 1)) + c);
-            cv[jj()] = act ? load_sc1(a.R[q + 1] + i) : 0ull;
-            if constexpr (CHECK) {
-                if (act && load_sc1(a.tag[q + 1] + i) != casc_tag(a.epoch)) ++mm;
-            }
+        const uint32_t x = (s * (uint32_t)K + j) * (uint32_t)(K - 1) + r - (r > j ? 1u : 0u);
+        const uint64_t i = C::template addr<q + 1>(w, x);
+        cv[jj()] = act ? load_sc1(a.R[q + 1] + i) : 0ull;
+        if constexpr (CHECK) {
+            if (act && load_sc1(a.tag[q + 1] + i) != casc_tag(a.epoch)) ++mm;
         }
     });
     Csa<planes_c(K)> cnt;
@@ -334,10 +327,7 @@ __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in,
             if (act) a.votes[((uint64_t)(s - a.ub) * K + r) * a.W + w] = rq;
             return;
         }
-        // CHECK injection (BA_CASC_CHECK=2) in the sigma-blocked kernel: the first
-        // sigma of the launch stores one stale tag
-        const bool stale = CHECK && LK && a.inject && w == 0 && s == a.rho0 && r == 0;
-        if (act) casc_put<N, ME, q, CHECK>(a, w, s * (uint32_t)K + r, rq, stale);
+        if (act) casc_put<N, ME, q, CHECK>(a, w, s * (uint32_t)K + r, rq);
         drain_stores();
         // arrive at sigma's parent (level q-2), or at the word's root counter
         constexpr uint32_t up_fan = (uint32_t)(L - (q - 1));  // children of a level q-2 slot
@@ -491,160 +481,11 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// k_cascade_sb<N, ME>: the sigma-blocked cascade (Q = me-3 >= 1).  A block owns
-// SPB whole level-(Q-1) slots sigma: all FAN = L-Q units below each of them
-// (G lanes per unit, units may straddle waves: every unit-level exchange is
-// behind a block barrier), so step Q -- R_Q[sigma.r] from the units'
-// R_{me-2} -- runs in the block on LDS, with no hand-off: one hop fewer per
-// fan-in chain, and the hand-offs left are the level-(Q-1) and higher steps
-// (L(L-1)... of them per word instead of |L_{Q-1}| * FAN).
-//   1. input-free draws (leaf diagonal lies, the unit's relay-chain pairs into
-//      its xch)                                  | inputs sliced; barrier
-//   2. relay chain, leaf block, transpose           barrier
-//   3. R_{me-2}[rho.x] = maj over the transpose -> kids (LDS); barrier
-//   4. step Q of each sigma by one wave (casc_step<Q, LK>): R_Q stored
-//      write-through, arrival at sigma's parent; the fan-in above continues
-//      through the global hand-offs (acquire + sc1 loads)
-// ---------------------------------------------------------------------------
-template <int LPS>
-constexpr int casc_spb() {  // sigmas per block: the fewest waves at the best lane efficiency, <= 8 waves
-    int best = 1;
-    double be = 0.0;
-    for (int k = 1; k * LPS <= 512; ++k) {
-        const int wv = (k * LPS + 63) / 64;
-        const double e = (double)(k * LPS) / (double)(wv * 64);
-        if (e > be + 1e-9) {
-            be = e;
-            best = k;
-        }
-    }
-    return best;
-}
-
-template <int N, int ME>
-struct CascSB {
-    using C = Casc<N, ME>;
-    static constexpr int L = C::L, S = C::S, G = C::G, GP = C::GP, Q = C::Q, NIN = C::NIN;
-    static_assert(Q >= 1, "k_cascade_sb: me >= 4");
-    static constexpr int FAN = L - Q;        // units per sigma (the level-Q step's receivers)
-    static constexpr int LPS = FAN * G;      // lanes per sigma
-    static constexpr int SPB = casc_spb<LPS>();
-    static constexpr int UPB = SPB * FAN;    // units per block
-    static constexpr int WAVES = (SPB * LPS + 63) / 64;
-    static constexpr int THREADS = 64 * WAVES;
-    static constexpr int NCALL = (G / 2 + 1) + (Q + 1);  // RelayPlan<N, Q+1, G>::CALLS
-    static constexpr int XW = 2 * NCALL;     // xch words per unit
-    static constexpr int SCR = 64;           // step scratch words per wave (relay xch, epilogue)
-    static_assert(3 * N + 1 <= SCR, "step scratch");
-    // sigmas per word >= 1 (a range of one h-hop subtree at h = Q holds one)
-    static constexpr uint32_t nw_max = (uint32_t)SPB + 1;
-    static constexpr uint32_t oPL = 0, oXCH = (nw_max * NIN + 1u) & ~1u;
-    static constexpr uint32_t oTR = oXCH + UPB * XW, oKID = oTR + UPB * G * GP;
-    static constexpr uint32_t oSCR = oKID + UPB * G, words = oSCR + WAVES * SCR;
-};
-
-template <int N, int ME, bool CHECK = false>
-__global__ __launch_bounds__((CascSB<N, ME>::THREADS)) void k_cascade_sb(CascArgs a) {
-    using B = CascSB<N, ME>;
-    constexpr int L = B::L, S = B::S, G = B::G, GP = B::GP, Q = B::Q, NIN = B::NIN, FAN = B::FAN;
-    constexpr int NPD = (S + 1) / 2;
-    using RP = RelayPlan<N, Q + 1, G>;
-    static_assert(RP::CALLS == B::NCALL, "relay calls");
-    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    // sigma units: a.units = W * a.rr sigmas (a.rr per word, from a.rho0)
-    const uint32_t RS = a.rr;
-    const uint32_t g0 = blockIdx.x * (uint32_t)B::SPB;
-    const uint32_t gend = min(g0 + (uint32_t)B::SPB, a.units);
-    const uint32_t wfirst = g0 / RS, nw = (gend - 1u) / RS - wfirst + 1u;
-    uint64_t* planes = lds + B::oPL;
-    const uint64_t gw0 = a.first_trial >> 6;
-    TrialCounts tc;
-    uint32_t mm = 0;
-    // this lane's (sigma, unit, leaf block)
-    const uint32_t su = t / (uint32_t)B::LPS, rem = t - su * (uint32_t)B::LPS;
-    const uint32_t ux = rem / (uint32_t)G, x = rem - ux * (uint32_t)G;
-    const uint32_t gs = g0 + su;
-    const bool act = su < (uint32_t)B::SPB && gs < a.units;
-    const uint32_t gsa = act ? gs : g0;
-    const uint32_t w = gsa / RS, sig = a.rho0 + (gsa - w * RS);  // level Q-1 slot
-    const uint32_t uxa = act ? ux : 0u, xa = act ? x : 0u;
-    const uint32_t rho = sig * (uint32_t)FAN + uxa;             // level Q slot
-    const uint64_t gw = gw0 + w;
-    const uint32_t sr = rho * (uint32_t)G + xa;                 // level me-2 slot
-    const uint32_t ul = act ? su * (uint32_t)FAN + ux : 0u;     // unit within the block
-    uint64_t* xch = lds + B::oXCH + ul * (uint32_t)B::XW;
-    uint64_t* tr = lds + B::oTR + ul * (uint32_t)(G * GP);
-    // 1. input-free draws
-    uint64_t lw[2 * NPD], mem = 0;
-    const RP rp(rho, rho * (uint32_t)G);
-    if (act) {
-        mem = a.members[sr];
-        lie_pairs<NPD>(a.seed, ME - 1, (sr * (uint32_t)S) >> 1, gw, lw);
-        relay_draw<N, Q + 1, G, G>(a, rp, xch, xa, true, gw);
-    }
-    for (uint32_t k = wv; k < nw; k += (uint32_t)B::WAVES)
-        wave_inputs<N, 1, 0>(planes + k * NIN, lane, wfirst + k, a.seed, a.gs, a.first_trial,
-                             a.ntrials, a.faulty, a.order);
-    __syncthreads();
-    // 2. relay chain, leaf block, transpose
-    const uint64_t* in = planes + (w - wfirst) * NIN;
-    if (act) {
-        uint32_t path[Q + 2], srt[Q + 2];
-        unrank_path<L, Q + 1>(sr, path, srt);
-        const uint64_t par = relay_apply<N, Q + 1, G>(rp, in, xch, xa, rho * (uint32_t)G, path);
-        const uint64_t fs = in[path[Q + 1] + 1];
-        const uint64_t oddmask = 0ull - (uint64_t)((sr * (uint32_t)S) & 1u);
-        uint64_t diag[S], Fm[S], Rm[S];
-        static_for<0, S>([&](auto b) {
-            uint64_t lie;
-            if constexpr (S % 2 == 1) lie = lw[b()] ^ ((lw[b()] ^ lw[b() + 1]) & oddmask);
-            else lie = lw[b()];
-            diag[b()] = sel64(fs, lie, par);
-            Fm[b()] = in[(mem >> (5 * b())) & 31u];
-        });
-        leaf_block<S>(ME, a.seed, gw, sr, diag, Fm, Rm);
-        uint64_t* tc_ = tr + xa;
-        tc_[xa * GP] = par;
-        static_for<0, S>([&](auto d) { tc_[(d() + (d() >= xa ? 1u : 0u)) * GP] = Rm[d()]; });
-    }
-    __syncthreads();
-    // 3. R_{me-2}[rho.x] = maj(L_{me-2}[rho.x], R_{me-1}[rho.a.x] : a != x) -> kids
-    if (act) {
-        const uint64_t* col = tr + xa * GP;
-        Csa<planes_c(G)> cnt;
-        static_for<0, G>([&](auto b) { cnt.template add<b()>(col[b()]); });
-        lds[B::oKID + ul * (uint32_t)G + xa] = cnt.template ge<G, G / 2 + 1>();
-    }
-    __syncthreads();
-    // 4. step Q of each of the block's sigmas, one wave each
-    uint64_t* scr = lds + B::oSCR + wv * (uint32_t)B::SCR;
-    for (uint32_t k = wv; k < (uint32_t)B::SPB; k += (uint32_t)B::WAVES) {
-        const uint32_t gk = g0 + k;
-        if (gk >= a.units) break;  // wave-uniform
-        const uint32_t wk = gk / RS, sk = a.rho0 + (gk - wk * RS);
-        casc_step<N, ME, Q, CHECK, true>(a, planes + (wk - wfirst) * NIN, scr, lane, wk, sk, gw0 + wk,
-                                         tc, mm, lds + B::oKID + k * (uint32_t)(FAN * G));
-    }
-    if constexpr (CHECK) {
-        uint32_t v = mm;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-        if (lane == 0 && v != 0 && a.counters)
-            atomicAdd((unsigned long long*)(a.counters + BA_C_CHECK_MISMATCH), (unsigned long long)v);
-    }
-    wave_flush<B::WAVES>(tc, lane, wv, (uint32_t)B::WAVES, a.counters, a.sk, a.counters == nullptr);
-}
-
-// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 #define BA_CASC_SHAPES(X) X(16, 5) X(16, 4) X(16, 3) X(10, 3) X(9, 4) X(8, 5)
 // CHECK builds (tests only): depth 5 at two fan-outs, and a root-only cascade
 #define BA_CASC_CHECK_SHAPES(X) X(16, 5) X(8, 5) X(10, 3)
-// the sigma-blocked kernel: the shapes above with me >= 4
-#define BA_CASC_SB_SHAPES(X) X(16, 5) X(16, 4) X(9, 4) X(8, 5)
-#define BA_CASC_SB_CHECK_SHAPES(X) X(16, 5) X(8, 5)
 
 bool cascade_supported(const Geometry& g) {
 #define BA_CASC_OK(nn, mm) if (g.n == nn && g.me == mm) return true;
@@ -674,22 +515,6 @@ bool cascade_range_supported(const Geometry& g, uint32_t h) {
     return cascade_supported(g) && (h == 1 || h == 2) && h + 3 <= g.me;
 }
 
-template <int N, int ME, bool CHECK = false>
-static hipError_t launch_cascade_sb_t(CascArgs& ca, hipStream_t st) {
-    using B = CascSB<N, ME>;
-    const uint32_t blocks = (ca.units + B::SPB - 1) / B::SPB;
-    hipLaunchKernelGGL((k_cascade_sb<N, ME, CHECK>), dim3(blocks ? blocks : 1), dim3(B::THREADS),
-                       (size_t)B::words * sizeof(uint64_t), st, ca);
-    return hipGetLastError();
-}
-
-// BA_CASC_SB=0 (read per call; A/B and cross-checks): the unit-wave kernel
-// k_cascade for every shape, where me >= 4 trees default to k_cascade_sb
-static bool use_sigma_blocks(const Geometry& g) {
-    const char* e = getenv("BA_CASC_SB");
-    return g.me >= 4 && !(e && e[0] == '0');
-}
-
 template <int N, int ME, int DIAG = 0, bool CHECK = false>
 static hipError_t launch_cascade_t(CascArgs& ca, hipStream_t st) {
     using C = Casc<N, ME>;
@@ -711,13 +536,11 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
     ca.first_trial = a.first_trial + trial0;
     ca.ntrials = ntrials;
     ca.W = (uint32_t)W;
-    // the units: level-Q slots (k_cascade) or level-(Q-1) slots sigma (k_cascade_sb)
-    const bool sb = use_sigma_blocks(g) && !getenv("BA_CASC_DIAG");
-    const uint64_t RQ = g.S[g.me - 3 - (sb ? 1 : 0)];
+    const uint64_t RQ = g.S[g.me - 3];
     if (job.h == 0) {
         ca.rr = (uint32_t)RQ;
         ca.rho0 = 0;
-    } else {  // the units below the h-hop subtrees [ub, ue)
+    } else {  // level-Q slots below the h-hop subtrees [ub, ue)
         const uint64_t per = RQ / g.S[job.h - 1];
         ca.rr = (uint32_t)((job.ue - job.ub) * per);
         ca.rho0 = (uint32_t)(job.ub * per);
@@ -752,21 +575,7 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
     ca.outcome = a.outcome ? a.outcome + trial0 : nullptr;
     ca.counters = job.h ? nullptr : a.counters;
     ca.sk = a.sink;
-    ProfScope ps(a.prof, sb ? "k_cascade_sb" : "k_cascade", a.stream);
-    if (sb) {
-        if (job.check) {
-#define BA_CASC_SB_CHECK_LAUNCH(nn, mm) \
-    if (g.n == nn && g.me == mm) return launch_cascade_sb_t<nn, mm, true>(ca, a.stream);
-            BA_CASC_SB_CHECK_SHAPES(BA_CASC_SB_CHECK_LAUNCH)
-#undef BA_CASC_SB_CHECK_LAUNCH
-            return hipErrorInvalidValue;
-        }
-#define BA_CASC_SB_LAUNCH(nn, mm) \
-    if (g.n == nn && g.me == mm) return launch_cascade_sb_t<nn, mm>(ca, a.stream);
-        BA_CASC_SB_SHAPES(BA_CASC_SB_LAUNCH)
-#undef BA_CASC_SB_LAUNCH
-        return hipErrorInvalidValue;
-    }
+    ProfScope ps(a.prof, "k_cascade", a.stream);
     if (const char* d = getenv("BA_CASC_DIAG")) {  // lab ablations, n=16 m=5 only
         if (g.n == 16 && g.me == 5 && job.h == 0 && !job.check) switch (atoi(d)) {
             case 2: return launch_cascade_t<16, 5, 2>(ca, a.stream);

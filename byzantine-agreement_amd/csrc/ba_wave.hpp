@@ -485,7 +485,6 @@ __device__ __forceinline__ void wave_flush_folded(uint64_t mine, uint32_t lane, 
 // Run counters of the block: wave sums (lane c holds counter c), the waves
 // combine in LDS, then one sink unit per block.  Every wave of the block
 // must call it (it contains a block barrier).
-template <int MAXW = kWaveThreads / 64>
 __device__ __forceinline__ void wave_flush(const TrialCounts& tc, uint32_t lane, uint32_t wv,
                                            uint32_t wpb, uint64_t* __restrict__ counters,
                                            const Sink& sk, bool skip) {
@@ -497,7 +496,7 @@ __device__ __forceinline__ void wave_flush(const TrialCounts& tc, uint32_t lane,
         for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
         if (lane == (uint32_t)c) mine = x;
     }
-    __shared__ unsigned long long wcnt[MAXW][16];
+    __shared__ unsigned long long wcnt[kWaveThreads / 64][16];
     if (lane < 16) wcnt[wv][lane] = mine;
     __syncthreads();
     if (wv == 0 && !skip) {

@@ -149,31 +149,3 @@ def test_cascade_handoff_detector_fires(engine, monkeypatch, n, m):
     monkeypatch.setenv("BA_CASC_CHECK", "2")
     mism, _, _ = _check_calls(engine, n, m, (1, 130), 6, 2)
     assert mism.tolist() == [1] * 6
-
-
-@pytest.mark.parametrize("n,m,B", [(16, 5, 1024), (16, 5, 1), (16, 5, 130), (16, 4, 200), (9, 4, 3000),
-                                   (8, 5, 700), (8, 5, 1)])
-def test_sigma_blocked_equals_unit_waves(engine, monkeypatch, n, m, B):
-    """k_cascade_sb (me >= 4 default: a block owns whole level-(me-4) slots and
-    runs their step in LDS) against k_cascade (BA_CASC_SB=0, one hand-off per
-    unit): same bits, and the oracle's; the profile names the kernel that ran."""
-    from ba_amd import lib as L
-    kw = dict(seed=0x5B + B, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1, order_mode=L.ORDER_RANDOM,
-              first_trial=64 * 5)
-    engine.profile(True)
-    a = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
-    prof = engine.profile_read()
-    engine.profile(False)
-    assert "k_cascade_sb" in prof, prof
-    monkeypatch.setenv("BA_CASC_SB", "0")
-    engine.profile(True)
-    b = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
-    prof = engine.profile_read()
-    engine.profile(False)
-    monkeypatch.delenv("BA_CASC_SB")
-    assert "k_cascade" in prof and "k_cascade_sb" not in prof, prof
-    same(a.decisions, b.decisions, "decisions")
-    same(a.outcome, b.outcome, "outcome")
-    assert a.counters == b.counters
-    if B <= 200 or (n, m) != (16, 5):
-        _check(a, n, m, B, **kw)
