@@ -354,7 +354,7 @@ def test_split_votes_single_units_through_cascade(engine, monkeypatch, n, m, lev
                     torch.cuda.synchronize()
                     prof = engine.profile_read()
                     engine.profile(False)
-                    assert ("k_cascade" in prof) == (casc == "1"), prof
+                    assert any("k_cascade" in k for k in prof) == (casc == "1"), prof
                     got[casc] = v.cpu().numpy().view(np.uint64)
                 assert np.array_equal(got["1"], oracle_c.pack_votes(v_or, ub, ue)), (B, ub, ue)
                 assert np.array_equal(got["1"], got["0"])

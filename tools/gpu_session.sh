@@ -59,10 +59,6 @@ for s in $STAGES; do
             run c5ab_1024_$t 300 env BA_HIP_LIB=$ROOT/$lib python -u tools/config5_prof.py --batch 1024 || exit $?
             run c5ab_1_$t 300 env BA_HIP_LIB=$ROOT/$lib python -u tools/config5_prof.py --batch 1 --reps 500 || exit $?
           done; done ;;
-    c5sb) for r in 1 2; do for sb in 1 0; do
-            run c5sb_1024_sb${sb}_$r 300 env BA_CASC_SB=$sb python -u tools/config5_prof.py --batch 1024 || exit $?
-            run c5sb_1_sb${sb}_$r 300 env BA_CASC_SB=$sb python -u tools/config5_prof.py --batch 1 --reps 500 || exit $?
-          done; done ;;
     casc) run pytest_casc 600 python -u -m pytest tests/test_gpu_cascade.py tests/test_dist.py -m gpu -v --timeout 200 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
     c5prof) for b in 1024 1; do
           (cd /tmp && export TMPDIR=/tmp && mkdir -p "$ROOT/gpurun_out/c5prof_$b" && \
