@@ -26,6 +26,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "byzantine-agreement_amd"))
+sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -231,6 +232,21 @@ def main():
                     "stream_note": "staged inputs, calls launched back to back on one stream; "
                                    "stream2: two calls in flight on two ctx streams (one rank only)",
                     "n_gpus": world, "counters_batch": res[a.batch5]["counters"]})
+        # the Philox roofline of the batch call on one stream (tools/config5_prof.py
+        # has the same figure per process, for rocprofv3 runs of one batch size)
+        sec = res[a.batch5].get("stream_seconds_per_call")
+        if sec:
+            import bench  # philox_calls_per_trial_word, philox_peaks
+            calls = bench.philox_calls_per_trial_word(n, m) * ((a.batch5 + 63) // 64)
+            peaks = bench.philox_peaks()
+            pk = peaks.get(2, max(peaks.values()))
+            out[-1]["compute_roofline"] = {
+                "bound": "valu (Philox4x32-10 lie draws, ba.py:42-57 at every relay level)",
+                "unit": "G Philox calls/s", "calls_per_call": calls,
+                "achieved": round(calls / sec / 1e9, 2), "peak": round(pk / 1e9, 2),
+                "peak_waves_per_simd": 2, "frac": round(calls / sec / pk, 4),
+                "floor_us": round(calls / pk * 1e6, 2), "peak_source": bench.PHILOX_PEAK_SRC,
+                "timing": "batch call on one stream (stream_seconds_per_call)"}
 
     if rank == 0:
         for line in out:
