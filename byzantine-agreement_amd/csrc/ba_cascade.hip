@@ -24,14 +24,13 @@
 // Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): results are
 // stored write-through (sc1: relaxed agent-scope atomic stores), the storing
 // wave drains vmcnt, then ONE lane per unit adds to the parent's counter (agent
-// scope); the wave whose add returns the last count takes an agent-scope
-// acquire (buffer_inv sc1: the guide's "Consumer, always" form, valid at any
-// number of workgroups per CU) and reads the children with sc1 loads.  The
-// children of one parent sit on 128-B lines of their own (each sigma's child
-// block is padded to whole lines, casc_pad), so no line a reader pulls in is
-// ever shared with a hand-off that is still being written.  Counters sit on
-// 128-B lines of their own; the last arriver resets its counter, so the buffer
-// is zero between calls (zeroed once when the ctx allocates it).
+// scope); the wave whose add returns the last count reads the children with
+// sc1 loads only (L2-served, never L1).  The children of one parent sit on
+// 128-B lines of their own (each sigma's child block is padded to whole lines,
+// casc_pad), so no line a reader pulls into its XCD's L2 is ever shared with a
+// hand-off still being written.  Counters sit on 128-B lines of their own; the
+// last arriver resets its counter, so the buffer is zero between calls (zeroed
+// once when the ctx allocates it).
 //
 // CHECK (test builds, BA_CASC_CHECK=1|2): every R store also stores a tag of
 // the call's epoch (sc1, parallel array), every child load also loads its tag,
@@ -270,10 +269,16 @@ __device__ __forceinline__ uint64_t relay_slots(const CascArgs& a, const uint64_
     return r;
 }
 
-// The arrival that completes a counter: an agent-scope acquire before the
-// children are read (BA_CASC_ACQUIRE=0: sc1 loads alone, A/B only).
+// The arrival that completes a counter may take an agent-scope acquire before
+// the children are read (-DBA_CASC_ACQUIRE=1, A/B builds).  Off by default:
+// the acquire invalidates this CU's L1 and nothing else (MI355X_MICROARCH.md,
+// fence table), and every child load is an sc1 load, which bypasses L1; with
+// the child blocks padded to lines of their own no L2 holds a line of a
+// hand-off before its reader loads it.  Measured cost of the acquire: +4.1 us
+// per 1024-instance n=16 m=5 call, +1.3 us per single instance
+// (profiles/r04a_acquire_ab.log).
 #ifndef BA_CASC_ACQUIRE
-#define BA_CASC_ACQUIRE 1
+#define BA_CASC_ACQUIRE 0
 #endif
 __device__ __forceinline__ void casc_acquire() {
 #if BA_CASC_ACQUIRE

@@ -82,6 +82,21 @@ def main():
         return {"wall": (t3 - t0) * 1e6, "enqueue": (t1 - t0) * 1e6, "poll": (t2 - t1) * 1e6,
                 "sync": (t3 - t2) * 1e6, "gpu": ev0.elapsed_time(ev1) * 1e3}
 
+    # bench.py's warm-up: >= 1 s of back-to-back steps on both streams, no
+    # cross-stream event waits; then the FIRST timed-region-shaped pass alone
+    t_w = time.perf_counter()
+    while time.perf_counter() - t_w < 1.0:
+        for i in range(K):
+            step(i)
+        torch.cuda.synchronize(dev)
+    first = region(K, False)
+    print(json.dumps({"variant": f"first_region_{K}_sync", "streams": NS,
+                      "us": {k: round(v, 1) for k, v in first.items()},
+                      "gap_us": round(first["wall"] - first["gpu"], 1)}), flush=True)
+    second = region(K, False)
+    print(json.dumps({"variant": f"second_region_{K}_sync", "streams": NS,
+                      "us": {k: round(v, 1) for k, v in second.items()},
+                      "gap_us": round(second["wall"] - second["gpu"], 1)}), flush=True)
     for _ in range(3):  # warm-up
         region(K)
     for name, ns, poll in (("empty", 0, True), (f"steps_{K}", K, True), (f"steps_{K}_sync", K, False),
