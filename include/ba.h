@@ -27,6 +27,10 @@
  *     captured from one ctx must not run concurrently with each other or with
  *     an eager call of that ctx: they share the ctx's scratch, counter sink
  *     and persistent-kernel task counter (one replay at a time per ctx).
+ *     Capture a ctx's calls only after an eager call of at least the same
+ *     size on that ctx: growing scratch or the LEVELS cascade's fan-in
+ *     counters allocates (and zeroes the counters on the call's stream),
+ *     which a capturing stream cannot do.
  *
  * General indexing: the live generals sorted by id are
  * indexed 0..n-1; index 0 is the commander (lowest live id, ba.py:381 +
