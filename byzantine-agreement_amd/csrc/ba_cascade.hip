@@ -357,9 +357,23 @@ __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in,
             scr[NIN + L + r] = tie;
         }
         __builtin_amdgcn_wave_barrier();
+        TrialCounts tw;
         wave_epilogue<N, 1, (uint32_t)ME, 0>(scr, scr + NIN, lane, w, a.ntrials, a.decisions,
-                                            a.outcome, tc);
+                                            a.outcome, tw);
         __builtin_amdgcn_wave_barrier();
+        // the word's counts, straight into the sink: every word's root step runs
+        // exactly once per launch, so the word is the sink's unit and no block
+        // barrier is needed to combine waves (a wave exits as soon as it is done)
+        uint64_t mine = 0;
+#pragma unroll
+        for (int c = 0; c < C_NUM; ++c) {
+            uint32_t x = tw.v[c];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+            if (lane == (uint32_t)c) mine = x;
+        }
+        if (a.counters) sink_counters(lane, mine, w, a.W, a.counters, a.sk);
+        (void)tc;
     }
 }
 
@@ -482,7 +496,7 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
         if (lane == 0 && t != 0 && a.counters)
             atomicAdd((unsigned long long*)(a.counters + BA_C_CHECK_MISMATCH), (unsigned long long)t);
     }
-    wave_flush(tc, lane, wv, kCascWaves, a.counters, a.sk, a.counters == nullptr);
+    // no end-of-block flush: the root steps put each word's counts into the sink
 }
 
 // ---------------------------------------------------------------------------
