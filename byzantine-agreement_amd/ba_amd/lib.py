@@ -43,7 +43,7 @@ EXPORTS = ["ba_version", "ba_device_count", "ba_ctx_create", "ba_ctx_destroy", "
            "ba_run_instance_split_multi", "ba_split_units", "ba_split_vote_slots",
            "ba_split_share", "ba_split_votes_device", "ba_root_from_split_votes_device",
            "ba_comm_allgather_split_votes_device", "ba_run_instance_split_level_multi",
-           "ba_clock_probe_device"]
+           "ba_clock_probe_device", "ba_ctx_memory"]
 PROBE_BLOCKS = 64  # BA_PROBE_BLOCKS
 
 
@@ -130,6 +130,7 @@ def load(path: str | None = None):
     lib.ba_ctx_device.argtypes = [vp, ctypes.POINTER(i32)]
     lib.ba_ctx_stream.argtypes = [vp, ctypes.POINTER(vp)]
     lib.ba_clock_probe_device.argtypes = [vp, vp, vp]
+    lib.ba_ctx_memory.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]
     lib.ba_comm_unique_id.argtypes = [ctypes.c_char_p]
     lib.ba_comm_create.argtypes = [vp, i32, i32, ctypes.c_char_p, ctypes.POINTER(vp)]
     lib.ba_comm_destroy.argtypes = [vp]
@@ -294,6 +295,14 @@ class Engine:
         _check(self.lib, self.lib.ba_subtree_votes_device(
             self.handle, ctypes.byref(params), batch, j_begin, j_end, d_faulty or None,
             d_order or None, d_votes, stream or None))
+
+    def memory(self) -> dict:
+        """Device bytes the ctx holds (ba_ctx_memory): LEVELS scratch, cascade fan-in
+        counters, and the budget they are chunked to."""
+        sc, cn, bu = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _check(self.lib, self.lib.ba_ctx_memory(self.handle, ctypes.byref(sc), ctypes.byref(cn),
+                                                ctypes.byref(bu)))
+        return {"scratch": sc.value, "counters": cn.value, "budget": bu.value}
 
     def clock_probe_device(self, d_out: int, stream=0):
         """Enqueue the engine-clock probe (ba_clock_probe_device): PROBE_BLOCKS rows of

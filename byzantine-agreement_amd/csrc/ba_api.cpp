@@ -393,6 +393,15 @@ extern "C" int ba_clock_probe_device(ba_ctx* ctx, uint64_t* d_out, void* stream)
     return BA_OK;
 }
 
+extern "C" int ba_ctx_memory(ba_ctx* ctx, uint64_t* scratch_bytes, uint64_t* counter_bytes,
+                             uint64_t* budget_bytes) {
+    if (!ctx) return fail(BA_EINVAL, "ctx is NULL");
+    if (scratch_bytes) *scratch_bytes = ctx->scratch.bytes;
+    if (counter_bytes) *counter_bytes = ctx->casc.bytes;
+    if (budget_bytes) *budget_bytes = ctx->scratch_budget;
+    return BA_OK;
+}
+
 extern "C" int ba_ctx_stream(ba_ctx* ctx, void** stream) {
     if (!ctx || !stream) return fail(BA_EINVAL, "ctx and stream are required");
     *stream = (void*)ctx->stream;

@@ -349,6 +349,13 @@ int ba_profile_read(struct ba_ctx* ctx, int index, char* name, int name_len,
  * probes bracketing a stretch of work give that stretch's average engine clock
  * per XCD: (dmemtime / drealtime) x 100 MHz (MI355X_MICROARCH.md).  bench.py
  * brackets a replica of its timed region with two probes. */
+/* Device memory a ctx holds for the engines: the LEVELS scratch and the
+ * cascade's fan-in counters, and the budget both are chunked to (environment
+ * BA_SCRATCH_BYTES at ba_ctx_create, 8 GiB by default): scratch + counters <=
+ * budget for every call the budget admits. */
+int ba_ctx_memory(struct ba_ctx* ctx, uint64_t* scratch_bytes, uint64_t* counter_bytes,
+                  uint64_t* budget_bytes);
+
 #define BA_PROBE_BLOCKS 64
 int ba_clock_probe_device(struct ba_ctx* ctx, uint64_t* d_out, void* stream);
 

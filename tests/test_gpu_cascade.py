@@ -149,3 +149,39 @@ def test_cascade_handoff_detector_fires(engine, monkeypatch, n, m):
     monkeypatch.setenv("BA_CASC_CHECK", "2")
     mism, _, _ = _check_calls(engine, n, m, (1, 130), 6, 2)
     assert mism.tolist() == [1] * 6
+
+
+@pytest.mark.parametrize("n,m,budget_words", [(8, 5, 3), (9, 4, 2), (16, 5, 1)])
+def test_cascade_scratch_budget_counts_counters(monkeypatch, n, m, budget_words):
+    """BA_SCRATCH_BYTES bounds the cascade's scratch AND its fan-in counter lines
+    together (round-3 advisor finding: the counters were allocated on top): with a
+    budget of a few words' worth, scratch + counters stay within it, the batch runs
+    in several chunks, and the results are the oracle's."""
+    from ba_amd import lib as L
+    # per 64-instance word: R_1..R_{me-2} (line-padded) + one 128-B counter per fan-in slot
+    lib = L.load()
+    me = L.effective_depth(n, m)
+    S = [lib.ba_level_slots(n, m, k) for k in range(me + 1)]
+    Lh = n - 1
+
+    def pad(k):
+        g = (Lh - k + 1) * (Lh - k)
+        return ((g + 15) // 16) * 16 * (S[k - 2] if k >= 2 else 1)
+    per_word = 8 * sum(pad(k) for k in range(1, me - 1)) + 128 * (1 + sum(S[k] for k in range(me - 3)))
+    budget = per_word * budget_words + per_word // 2
+    monkeypatch.setenv("BA_SCRATCH_BYTES", str(budget))
+    eng = L.Engine(0)
+    try:
+        B = 64 * (budget_words * 3 + 1) + 17
+        kw = dict(seed=0xB0D6E7 + n, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3,
+                  order_mode=L.ORDER_RANDOM, first_trial=64 * 2)
+        eng.profile(True)
+        res = eng.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
+        prof = eng.profile_read()
+        mem = eng.memory()
+        assert mem["budget"] == budget
+        assert 0 < mem["scratch"] + mem["counters"] <= budget, mem
+        assert prof["k_cascade"][0] >= 3, prof  # chunked
+        _check(res, n, m, B, **kw)
+    finally:
+        eng.close()
