@@ -617,7 +617,8 @@ static uint32_t cascade_check_mode(const Geometry& g) {
 // job.h != 0 (the subtree split): one chunk (`whole`), no counters.
 static int run_cascade(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge, CascJob job = CascJob{}) {
     const Geometry& g = ge->g;
-    job.check = job.h ? 0u : cascade_check_mode(g);
+    const bool whole = job.h != 0 || job.vin != nullptr;  // vote rows span the whole batch
+    job.check = whole ? 0u : cascade_check_mode(g);
     // per trial word: R_1 .. R_{me-2} (twice with check tags) and the fan-in
     // counters, one 128-B line each -- both count against the scratch budget
     const uint64_t r_bytes = cascade_scratch_words_per_word(g) * sizeof(uint64_t) * (job.check ? 2 : 1);
@@ -629,10 +630,10 @@ static int run_cascade(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge, CascJob job 
     const uint64_t idx_cap = (1ull << 31) / (max_level + 1);  // 32-bit slot indices in the kernel
     if (chunk > idx_cap) chunk = idx_cap;
     if (chunk > words) chunk = words;
-    if (chunk == 0 || (job.h && chunk < words))
+    if (chunk == 0 || (whole && chunk < words))
         return fail(BA_ETOOBIG, "%llu 64-trial words need %llu bytes of scratch and counters each "
                     "(budget %zu%s)", (unsigned long long)words, (unsigned long long)(r_bytes + c_bytes),
-                    ctx->scratch_budget, job.h ? ", one chunk required: split the batch" : "");
+                    ctx->scratch_budget, whole ? ", one chunk required: split the batch" : "");
     int rc;
     if ((rc = ctx->scratch.grow(chunk * r_bytes)) != BA_OK) return rc;
     const size_t cbytes = chunk * c_bytes;
@@ -797,6 +798,12 @@ static int root_from_votes_impl(ba_ctx* ctx, const ba_params* p, uint64_t batch,
     GeoEntry* ge = geometry(ctx, a.n, a.me, &rc);
     if (!ge) return rc;
     a.members = (const uint64_t*)ge->members.p;
+    if (use_cascade(ctx, ge->g) && cascade_range_supported(ge->g, level)) {
+        CascJob cj;  // one launch: step level-1 from the votes, roots, quorum
+        cj.vin = d_votes;
+        cj.root_h = level;
+        return run_cascade(ctx, a, ge, cj);
+    }
     LevelsJob job;
     job.tree = false;
     job.h = level;

@@ -89,6 +89,7 @@ struct CascArgs {
     uint32_t h;           // range mode: the vote level (1 or 2); 0 = whole tree
     uint32_t ub;          // range mode: first h-hop subtree of the range
     uint64_t* votes;      // range mode: [(u - ub)(L - h) + c][W]
+    const uint64_t* vin;  // root mode: every unit's votes, [level-h slot][W]
     uint64_t* decisions;  // chunk-relative
     uint8_t* outcome;
     uint64_t* counters;   // nullptr in range mode
@@ -299,7 +300,10 @@ __device__ __forceinline__ void casc_put(const CascArgs& a, uint32_t w, uint32_t
 // whole wave, lane r = receiver index among the K = L - q lieutenants not in
 // sigma.  in: the word's input planes (LDS); scr: the wave's LDS scratch.
 // mm: CHECK builds' per-lane count of child tags that were not this launch's.
-template <int N, int ME, int q, bool CHECK>
+// VIN: the children are rows of the gathered vote array a.vin (the root pass of
+// the subtree split: written by an earlier launch / RCCL, plain loads), not a
+// hand-off of this launch.
+template <int N, int ME, int q, bool CHECK, bool VIN = false>
 __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in, uint64_t* scr,
                                           uint32_t lane, uint32_t w, uint32_t s, uint64_t gw,
                                           TrialCounts& tc, uint32_t& mm) {
@@ -317,10 +321,14 @@ __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in,
     static_for<0, K - 1>([&](auto jj) {
         const uint32_t j = (uint32_t)jj() + ((uint32_t)jj() >= r ? 1u : 0u);
         const uint32_t x = (s * (uint32_t)K + j) * (uint32_t)(K - 1) + r - (r > j ? 1u : 0u);
-        const uint64_t i = C::template addr<q + 1>(w, x);
-        cv[jj()] = act ? load_sc1(a.R[q + 1] + i) : 0ull;
-        if constexpr (CHECK) {
-            if (act && load_sc1(a.tag[q + 1] + i) != casc_tag(a.epoch)) ++mm;
+        if constexpr (VIN) {  // vote row = level-(q+1) slot, W words per row
+            cv[jj()] = act ? a.vin[(uint64_t)x * a.W + w] : 0ull;
+        } else {
+            const uint64_t i = C::template addr<q + 1>(w, x);
+            cv[jj()] = act ? load_sc1(a.R[q + 1] + i) : 0ull;
+            if constexpr (CHECK) {
+                if (act && load_sc1(a.tag[q + 1] + i) != casc_tag(a.epoch)) ++mm;
+            }
         }
     });
     Csa<planes_c(K)> cnt;
@@ -500,9 +508,42 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// k_cascade_root<N, ME, H>: the root pass of the subtree split in ONE launch.
+// Every unit's level-H votes are gathered in a.vin; one wave per (word, level
+// H-2 slot sigma) -- H = 2: the word's L first hops, H = 1: the word itself --
+// slices its word's inputs, relays L_{H-1}[sigma.r] and takes step H-1 with
+// the votes as children; at H = 2 the R_1 results are handed off (sc1, padded,
+// as in k_cascade) to the root step of the word's last arriver, which runs the
+// roots and the quorum epilogue (ba.py:159-255) and feeds the counter sink.
+// Waves never wait for each other and there is no block barrier.
+// ---------------------------------------------------------------------------
+template <int N, int ME, int H>
+__global__ __launch_bounds__(64 * kCascWaves) void k_cascade_root(CascArgs a) {
+    using C = Casc<N, ME>;
+    static_assert(H == 1 || H == 2, "split levels 1 and 2");
+    constexpr int L = C::L, NIN = C::NIN;
+    constexpr uint32_t PER = H == 2 ? (uint32_t)L : 1u;  // waves per word
+    constexpr uint32_t WS = 64;                           // step scratch words per wave
+    __shared__ __attribute__((aligned(16))) uint64_t sh[kCascWaves][((NIN + 1) & ~1) + WS];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t u = blockIdx.x * kCascWaves + wv;
+    if (u >= a.units) return;  // wave-uniform; no barrier follows
+    const uint32_t w = u / PER, sg = u - w * PER;
+    uint64_t* planes = sh[wv];
+    uint64_t* scr = sh[wv] + ((NIN + 1) & ~1);
+    wave_inputs<N, 1, 0>(planes, lane, w, a.seed, a.gs, a.first_trial, a.ntrials, a.faulty, a.order);
+    __builtin_amdgcn_wave_barrier();
+    TrialCounts tc;
+    uint32_t mm = 0;
+    casc_step<N, ME, H - 1, false, true>(a, planes, scr, lane, w, sg, (a.first_trial >> 6) + w, tc, mm);
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 #define BA_CASC_SHAPES(X) X(16, 5) X(16, 4) X(16, 3) X(10, 3) X(9, 4) X(8, 5)
+// shapes whose subtree split (h <= me-3) runs through the cascade (range and root modes)
+#define BA_CASC_RANGE_SHAPES(X) X(16, 5) X(16, 4) X(9, 4) X(8, 5)
 // CHECK builds (tests only): depth 5 at two fan-outs, and a root-only cascade
 #define BA_CASC_CHECK_SHAPES(X) X(16, 5) X(8, 5) X(10, 3)
 
@@ -531,7 +572,11 @@ uint64_t cascade_scratch_words_per_word(const Geometry& g) {
 // the subtree split through the cascade: h-hop subtrees need h <= me-3 (the
 // vote step is a fan-in step, not the units' own level)
 bool cascade_range_supported(const Geometry& g, uint32_t h) {
-    return cascade_supported(g) && (h == 1 || h == 2) && h + 3 <= g.me;
+    bool shape = false;
+#define BA_CASC_OK(nn, mm) if (g.n == nn && g.me == mm) shape = true;
+    BA_CASC_RANGE_SHAPES(BA_CASC_OK)
+#undef BA_CASC_OK
+    return shape && (h == 1 || h == 2) && h + 3 <= g.me;
 }
 
 template <int N, int ME, int DIAG = 0, bool CHECK = false>
@@ -594,6 +639,27 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
     ca.outcome = a.outcome ? a.outcome + trial0 : nullptr;
     ca.counters = job.h ? nullptr : a.counters;
     ca.sk = a.sink;
+    if (job.vin) {  // the split's root pass: one wave per (word, level root_h-2 slot)
+        ca.vin = job.vin;
+        ca.h = 0;
+        ca.units = (uint32_t)(W * (job.root_h == 2 ? g.L : 1u));
+        ca.counters = a.counters;
+        ProfScope ps(a.prof, "k_cascade_root", a.stream);
+        const uint32_t blocks = (ca.units + kCascWaves - 1) / kCascWaves;
+#define BA_CASC_ROOT_LAUNCH(nn, mm)                                                                  \
+    if (g.n == nn && g.me == mm) {                                                                 \
+        if (job.root_h == 2)                                                                       \
+            hipLaunchKernelGGL((k_cascade_root<nn, mm, 2>), dim3(blocks), dim3(64 * kCascWaves), 0,  \
+                               a.stream, ca);                                                      \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_cascade_root<nn, mm, 1>), dim3(blocks), dim3(64 * kCascWaves), 0,  \
+                               a.stream, ca);                                                      \
+        return hipGetLastError();                                                                  \
+    }
+        BA_CASC_RANGE_SHAPES(BA_CASC_ROOT_LAUNCH)
+#undef BA_CASC_ROOT_LAUNCH
+        return hipErrorInvalidValue;
+    }
     ProfScope ps(a.prof, "k_cascade", a.stream);
     if (const char* d = getenv("BA_CASC_DIAG")) {  // lab ablations, n=16 m=5 only
         if (g.n == 16 && g.me == 5 && job.h == 0 && !job.check) switch (atoi(d)) {

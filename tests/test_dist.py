@@ -247,16 +247,20 @@ def test_oracle_votes_reproduce_root_decisions():
 
 # --- GPU: the real entries ---------------------------------------------------------
 @pytest.mark.gpu
+@pytest.mark.parametrize("nocasc", ["0", "1"])
 @pytest.mark.parametrize("n,m,B,nr", [(10, 3, 200, 4), (7, 1, 100, 4), (9, 2, 130, 4), (16, 5, 2, 4),
                                       # odd n at depth 3: a first-hop subtree holds an odd
                                       # number of level-1 slots, so with 3 ranks a range
                                       # starts mid slot pair (k_relay_top's range edges)
                                       (9, 3, 150, 3), (5, 3, 70, 3), (13, 3, 65, 5),
-                                      (16, 5, 70, 8)])
-def test_subtree_votes_match_oracle_gpu(engine, n, m, B, nr):
+                                      (16, 5, 70, 8), (9, 4, 200, 3), (16, 4, 66, 6)])
+def test_subtree_votes_match_oracle_gpu(engine, monkeypatch, n, m, B, nr, nocasc):
     """Every rank's ba_subtree_votes_device rows (ranges from ba_subtree_share) equal
-    the oracle's, and the root pass over the assembled rows equals the oracle's run."""
+    the oracle's, and the root pass over the assembled rows equals the oracle's run
+    (the cascade's range and root modes on its shapes; BA_NO_CASCADE=1: the
+    multi-launch LEVELS kernels)."""
     from ba_amd import lib as L
+    monkeypatch.setenv("BA_NO_CASCADE", nocasc)
     dev = torch.device("cuda", 0)
     kw = dict(seed=11, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1, order_mode=L.ORDER_RANDOM,
               first_trial=64 * 3)
@@ -284,13 +288,17 @@ def test_subtree_votes_match_oracle_gpu(engine, n, m, B, nr):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nocasc", ["0", "1"])
 @pytest.mark.parametrize("n,m,B,nr", [(10, 3, 200, 4), (9, 4, 130, 3), (13, 4, 65, 5),
-                                      (7, 3, 100, 3), (16, 5, 2, 8), (16, 5, 70, 8)])
-def test_second_hop_votes_match_oracle_gpu(engine, n, m, B, nr):
+                                      (7, 3, 100, 3), (16, 5, 2, 8), (16, 5, 70, 8), (8, 5, 300, 5)])
+def test_second_hop_votes_match_oracle_gpu(engine, monkeypatch, n, m, B, nr, nocasc):
     """Second-hop split (ba_split_votes_device, level 2): every rank's R_2 rows
     (ranges from ba_split_share, starting mid first-hop subtree) equal the
-    oracle's, and the root pass over the assembled rows equals the oracle's run."""
+    oracle's, and the root pass over the assembled rows equals the oracle's run --
+    through the cascade (range-mode votes, k_cascade_root) where the shape has it,
+    and through the multi-launch LEVELS kernels (BA_NO_CASCADE=1)."""
     from ba_amd import lib as L
+    monkeypatch.setenv("BA_NO_CASCADE", nocasc)
     dev = torch.device("cuda", 0)
     kw = dict(seed=13, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1, order_mode=L.ORDER_RANDOM,
               first_trial=64 * 5)
