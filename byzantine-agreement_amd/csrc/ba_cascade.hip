@@ -425,6 +425,16 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
     const uint32_t sr = rho * (uint32_t)G + x;  // the lane's level me-2 slot
     const uint32_t gg = act ? g : 0u;
     uint64_t* xch = tr + gg * (G * GP);  // the unit's relay exchange (before its transpose)
+    // 0. staged inputs: the loads of this wave's word go out first, so the draws
+    //    below hide their latency
+    const bool staged = a.gs.faulty_mode == 0 && a.gs.order_mode == 0;
+    uint32_t pfm = 0, poc = 0;
+    const uint64_t pi = (uint64_t)(wfirst + wv) * 64 + lane;
+    const bool pv = staged && wv < nw && pi < a.ntrials;
+    if (pv) {
+        pfm = a.faulty[pi];
+        poc = a.order[pi];
+    }
     // 1. input-free draws
     uint64_t lw[2 * NPD], mem = 0;
     const RP rp(rho, rho * (uint32_t)G);
@@ -434,9 +444,16 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
         relay_draw<N, Q + 1, G, G>(a, rp, xch, x, true, gw);
     }
     // 2. inputs
-    for (uint32_t k = wv; k < nw; k += kCascWaves)
-        wave_inputs<N, 1, 0>(planes + k * NIN, lane, wfirst + k, a.seed, a.gs, a.first_trial,
-                             a.ntrials, a.faulty, a.order);
+    if (staged) {
+        if (wv < nw) stage_slice<N>(planes + wv * NIN, lane, pfm, poc, pv);
+        for (uint32_t k = wv + kCascWaves; k < nw; k += kCascWaves)  // blocks spanning > 4 words
+            wave_inputs<N, 1, 0>(planes + k * NIN, lane, wfirst + k, a.seed, a.gs, a.first_trial,
+                                 a.ntrials, a.faulty, a.order);
+    } else {
+        for (uint32_t k = wv; k < nw; k += kCascWaves)
+            wave_inputs<N, 1, 0>(planes + k * NIN, lane, wfirst + k, a.seed, a.gs, a.first_trial,
+                                 a.ntrials, a.faulty, a.order);
+    }
     __syncthreads();
     // 3. the units (the leaf work sits in a divergent branch: as straight-line
     //    code for every lane the compiler's schedule needed 256 VGPRs and spilled)

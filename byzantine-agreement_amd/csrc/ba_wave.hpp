@@ -182,12 +182,31 @@ __device__ __forceinline__ void writelane4(uint32_t& lo, uint32_t& hi, const uin
     (void)l1; (void)h1; (void)l2; (void)h2; (void)l3; (void)h3;
 }
 
+// One word's staged inputs (this lane's trial: faulty mask fm, order code oc,
+// live v) -> the word's N+3 bit-sliced planes in0[0..N+3): one ballot per
+// plane, plane g dropped into lane g by v_writelane.
+template <int N>
+__device__ __forceinline__ void stage_slice(uint64_t* in0, uint32_t lane, uint32_t fm, uint32_t c,
+                                            bool v) {
+    constexpr int NIN = N + 3;
+    constexpr uint32_t FMASK = N >= 32 ? 0xFFFFFFFFu : ((1u << N) - 1u);
+    const uint32_t x = (fm & FMASK) | (c == 1u ? 1u << N : 0u) | (c == 2u ? 2u << N : 0u) |
+                       (v ? 4u << N : 0u);
+    uint32_t lo = 0, hi = 0;
+    static_for<0, (NIN + 3) / 4>([&](auto grp) {
+        constexpr int g0 = 4 * grp();
+        uint64_t b[4];
+        static_for<0, 4>([&](auto j) { b[j()] = g0 + j() < NIN ? __ballot((x >> (g0 + j())) & 1u) : 0ull; });
+        writelane4<g0, (NIN - g0 < 4 ? NIN - g0 : 4)>(lo, hi, b);
+    });
+    if (lane < (uint32_t)NIN) in0[lane] = (uint64_t)hi << 32 | lo;
+}
+
 template <int N, int W>
 __device__ __forceinline__ void stage_words(uint64_t* in0, uint32_t lane, uint64_t w0, uint64_t batch,
                                             const uint32_t* __restrict__ faulty,
                                             const uint8_t* __restrict__ order) {
     constexpr int NIN = N + 3;
-    constexpr uint32_t FMASK = N >= 32 ? 0xFFFFFFFFu : ((1u << N) - 1u);
     uint32_t fm[W], oc[W];
     static_for<0, W>([&](auto q) {
         const uint64_t i = (w0 + q()) * 64 + lane;
@@ -196,18 +215,7 @@ __device__ __forceinline__ void stage_words(uint64_t* in0, uint32_t lane, uint64
         oc[q()] = v ? (uint32_t)order[i] : 0u;
     });
     static_for<0, W>([&](auto q) {
-        const uint32_t c = oc[q()];
-        const bool v = (w0 + q()) * 64 + lane < batch;
-        const uint32_t x = (fm[q()] & FMASK) | (c == 1u ? 1u << N : 0u) | (c == 2u ? 2u << N : 0u) |
-                           (v ? 4u << N : 0u);
-        uint32_t lo = 0, hi = 0;
-        static_for<0, (NIN + 3) / 4>([&](auto grp) {
-            constexpr int g0 = 4 * grp();
-            uint64_t b[4];
-            static_for<0, 4>([&](auto j) { b[j()] = g0 + j() < NIN ? __ballot((x >> (g0 + j())) & 1u) : 0ull; });
-            writelane4<g0, (NIN - g0 < 4 ? NIN - g0 : 4)>(lo, hi, b);
-        });
-        if (lane < (uint32_t)NIN) in0[q() * NIN + lane] = (uint64_t)hi << 32 | lo;
+        stage_slice<N>(in0 + q() * NIN, lane, fm[q()], oc[q()], (w0 + q()) * 64 + lane < batch);
     });
 }
 
