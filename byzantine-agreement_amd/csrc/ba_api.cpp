@@ -605,6 +605,8 @@ static bool use_cascade(ba_ctx* ctx, const Geometry& g) {
     return !off && ctx->leaf_fusion && leaf_supported(g) && g.me >= 3 && cascade_supported(g);
 }
 
+constexpr uint64_t kCascTwoWords = 8;
+
 // BA_CASC_CHECK (tests only, read per call): 1 = the cascade's check build
 // (epoch tags beside every hand-off word, mismatches counted into
 // BA_C_CHECK_MISMATCH), 2 = the same with one stale tag injected.
@@ -619,6 +621,13 @@ static int run_cascade(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge, CascJob job 
     const Geometry& g = ge->g;
     const bool whole = job.h != 0 || job.vin != nullptr;  // vote rows span the whole batch
     job.check = whole ? 0u : cascade_check_mode(g);
+    // Two launches (units, then the fan-in) from kCascTwoWords 64-trial words on:
+    // the steps' latency-bound waves then no longer hold the slots the units use
+    // (DESIGN.md §4).  BA_CASC_TWO=0/1 (read per call) forces one or two.
+    if (!whole && g.me >= 4) {
+        const char* e = getenv("BA_CASC_TWO");
+        job.two = e ? atoi(e) != 0 : (a.batch + 63) / 64 >= kCascTwoWords;
+    }
     // per trial word: R_1 .. R_{me-2} (twice with check tags) and the fan-in
     // counters, one 128-B line each -- both count against the scratch budget
     const uint64_t r_bytes = cascade_scratch_words_per_word(g) * sizeof(uint64_t) * (job.check ? 2 : 1);

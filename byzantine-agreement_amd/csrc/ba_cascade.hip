@@ -397,8 +397,10 @@ __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in,
 // (A persistent, software-pipelined variant that deferred every drain and
 // arrival by one block-iteration measured slower: 97.6 vs 74.6 us for n=16,
 // m=5 at 1024 instances, at 207 VGPRs = 2 waves per SIMD.)
-// DIAG (lab only, tools/casc_lab.py, BA_CASC_DIAG; wrong results): 2 = no
-// fan-in (units only), 4 = arrivals but no steps.  The product uses 0.
+// DIAG: 2 = units only, no fan-in (the first launch of the two-launch mode,
+// k_cascade_top does the fan-in; alone: the lab's units-only ablation), 4 =
+// arrivals but no steps (lab only, tools/casc_lab.py, BA_CASC_DIAG; wrong
+// results).  The one-launch product uses 0.
 template <int N, int ME, int DIAG = 0, bool CHECK = false>
 __global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
     using C = Casc<N, ME>;
@@ -525,22 +527,25 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// k_cascade_root<N, ME, H>: the root pass of the subtree split in ONE launch.
-// Every unit's level-H votes are gathered in a.vin; one wave per (word, level
-// H-2 slot sigma) -- H = 2: the word's L first hops, H = 1: the word itself --
-// slices its word's inputs, relays L_{H-1}[sigma.r] and takes step H-1 with
-// the votes as children; at H = 2 the R_1 results are handed off (sc1, padded,
-// as in k_cascade) to the root step of the word's last arriver, which runs the
-// roots and the quorum epilogue (ba.py:159-255) and feeds the counter sink.
-// Waves never wait for each other and there is no block barrier.
+// k_cascade_top<N, ME, QS, VIN>: the fan-in from level QS up, in ONE launch,
+// over children an earlier launch (or RCCL) wrote.  One wave per (word,
+// level-(QS-1) slot sigma; QS = 0: the word) slices its word's inputs, relays
+// L_QS[sigma.r] and takes step QS (casc_step); the levels above hand off as in
+// k_cascade, and each word's root step runs the roots, the quorum epilogue
+// (ba.py:159-255) and feeds the counter sink.  No wave waits for another and
+// there is no block barrier.
+//   VIN = true: the subtree split's root pass -- the children are the gathered
+//     vote rows a.vin (QS = h-1).
+//   VIN = false: the two-launch cascade -- the children are R_{QS+1} from a
+//     units-only k_cascade launch (QS = me-3): the latency-bound steps no
+//     longer hold wave slots that the compute-bound units could use.
 // ---------------------------------------------------------------------------
-template <int N, int ME, int H>
-__global__ __launch_bounds__(64 * kCascWaves) void k_cascade_root(CascArgs a) {
+template <int N, int ME, int QS, bool VIN, bool CHECK = false>
+__global__ __launch_bounds__(64 * kCascWaves) void k_cascade_top(CascArgs a) {
     using C = Casc<N, ME>;
-    static_assert(H == 1 || H == 2, "split levels 1 and 2");
-    constexpr int L = C::L, NIN = C::NIN;
-    constexpr uint32_t PER = H == 2 ? (uint32_t)L : 1u;  // waves per word
-    constexpr uint32_t WS = 64;                           // step scratch words per wave
+    constexpr int NIN = C::NIN;
+    constexpr uint32_t PER = QS >= 1 ? C::sz(QS - 1) : 1u;  // waves per word
+    constexpr uint32_t WS = 64;                              // step scratch words per wave
     __shared__ __attribute__((aligned(16))) uint64_t sh[kCascWaves][((NIN + 1) & ~1) + WS];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t u = blockIdx.x * kCascWaves + wv;
@@ -552,15 +557,24 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade_root(CascArgs a) {
     __builtin_amdgcn_wave_barrier();
     TrialCounts tc;
     uint32_t mm = 0;
-    casc_step<N, ME, H - 1, false, true>(a, planes, scr, lane, w, sg, (a.first_trial >> 6) + w, tc, mm);
+    casc_step<N, ME, QS, CHECK, VIN>(a, planes, scr, lane, w, sg, (a.first_trial >> 6) + w, tc, mm);
+    if constexpr (CHECK) {
+        uint32_t t = mm;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+        if (lane == 0 && t != 0 && a.counters)
+            atomicAdd((unsigned long long*)(a.counters + BA_C_CHECK_MISMATCH), (unsigned long long)t);
+    }
 }
 
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 #define BA_CASC_SHAPES(X) X(16, 5) X(16, 4) X(16, 3) X(10, 3) X(9, 4) X(8, 5)
-// shapes whose subtree split (h <= me-3) runs through the cascade (range and root modes)
+// shapes whose subtree split (h <= me-3) runs through the cascade (range and root modes),
+// and that have the two-launch mode (me >= 4)
 #define BA_CASC_RANGE_SHAPES(X) X(16, 5) X(16, 4) X(9, 4) X(8, 5)
+#define BA_CASC_TWO_SHAPES(X) X(16, 5) X(16, 4) X(9, 4) X(8, 5)
 // CHECK builds (tests only): depth 5 at two fan-outs, and a root-only cascade
 #define BA_CASC_CHECK_SHAPES(X) X(16, 5) X(8, 5) X(10, 3)
 
@@ -661,20 +675,51 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
         ca.h = 0;
         ca.units = (uint32_t)(W * (job.root_h == 2 ? g.L : 1u));
         ca.counters = a.counters;
-        ProfScope ps(a.prof, "k_cascade_root", a.stream);
+        ProfScope ps(a.prof, "k_cascade_top", a.stream);
         const uint32_t blocks = (ca.units + kCascWaves - 1) / kCascWaves;
-#define BA_CASC_ROOT_LAUNCH(nn, mm)                                                                  \
-    if (g.n == nn && g.me == mm) {                                                                 \
-        if (job.root_h == 2)                                                                       \
-            hipLaunchKernelGGL((k_cascade_root<nn, mm, 2>), dim3(blocks), dim3(64 * kCascWaves), 0,  \
-                               a.stream, ca);                                                      \
-        else                                                                                       \
-            hipLaunchKernelGGL((k_cascade_root<nn, mm, 1>), dim3(blocks), dim3(64 * kCascWaves), 0,  \
-                               a.stream, ca);                                                      \
-        return hipGetLastError();                                                                  \
+#define BA_CASC_ROOT_LAUNCH(nn, mm)                                                                    \
+    if (g.n == nn && g.me == mm) {                                                                   \
+        if (job.root_h == 2)                                                                         \
+            hipLaunchKernelGGL((k_cascade_top<nn, mm, 1, true>), dim3(blocks), dim3(64 * kCascWaves), \
+                               0, a.stream, ca);                                                     \
+        else                                                                                         \
+            hipLaunchKernelGGL((k_cascade_top<nn, mm, 0, true>), dim3(blocks), dim3(64 * kCascWaves), \
+                               0, a.stream, ca);                                                     \
+        return hipGetLastError();                                                                    \
     }
         BA_CASC_RANGE_SHAPES(BA_CASC_ROOT_LAUNCH)
 #undef BA_CASC_ROOT_LAUNCH
+        return hipErrorInvalidValue;
+    }
+    if (job.two && job.h == 0 && g.me >= 4) {
+        // two launches: the units (k_cascade, DIAG 2: no fan-in), then the fan-in
+        // from level me-3 up (k_cascade_top), one wave per level-(me-4) slot
+        {
+            ProfScope ps(a.prof, "k_cascade_units", a.stream);
+            hipError_t e = hipErrorInvalidValue;
+#define BA_CASC_UNITS_LAUNCH(nn, mm) \
+    if (g.n == nn && g.me == mm) e = job.check ? launch_cascade_t<nn, mm, 2, true>(ca, a.stream) \
+                                               : launch_cascade_t<nn, mm, 2>(ca, a.stream);
+            BA_CASC_TWO_SHAPES(BA_CASC_UNITS_LAUNCH)
+#undef BA_CASC_UNITS_LAUNCH
+            if (e != hipSuccess) return e;
+        }
+        CascArgs ct = ca;
+        ct.units = (uint32_t)(W * g.S[g.me - 4]);
+        ProfScope ps(a.prof, "k_cascade_top", a.stream);
+        const uint32_t blocks = (ct.units + kCascWaves - 1) / kCascWaves;
+#define BA_CASC_TOP_LAUNCH(nn, mm)                                                                      \
+    if (g.n == nn && g.me == mm) {                                                                    \
+        if (job.check)                                                                                \
+            hipLaunchKernelGGL((k_cascade_top<nn, mm, mm - 3, false, true>), dim3(blocks),              \
+                               dim3(64 * kCascWaves), 0, a.stream, ct);                               \
+        else                                                                                          \
+            hipLaunchKernelGGL((k_cascade_top<nn, mm, mm - 3, false>), dim3(blocks),                    \
+                               dim3(64 * kCascWaves), 0, a.stream, ct);                               \
+        return hipGetLastError();                                                                     \
+    }
+        BA_CASC_TWO_SHAPES(BA_CASC_TOP_LAUNCH)
+#undef BA_CASC_TOP_LAUNCH
         return hipErrorInvalidValue;
     }
     ProfScope ps(a.prof, "k_cascade", a.stream);

@@ -159,6 +159,7 @@ struct CascJob {
     uint64_t* votes = nullptr;    // range mode: [(u - ub)(L - h) + c][W] (ba.h, ba_split_votes_device)
     const uint64_t* vin = nullptr;  // root mode: every unit's level-root_h votes (k_cascade_root)
     uint32_t root_h = 0;
+    bool two = false;               // two launches: units, then the fan-in (k_cascade_top)
     uint32_t check = 0;           // tests: 1 = epoch tags checked, 2 = and one stale tag injected
     uint64_t epoch = 0;           // check: this launch's tag
 };

@@ -185,3 +185,39 @@ def test_cascade_scratch_budget_counts_counters(monkeypatch, n, m, budget_words)
         _check(res, n, m, B, **kw)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("n,m,B", [(16, 5, 1024), (16, 5, 70), (16, 4, 600), (9, 4, 3000), (8, 5, 700),
+                                   (8, 5, 1)])
+def test_two_launch_equals_one_launch(engine, monkeypatch, n, m, B):
+    """BA_CASC_TWO=1 (units in one launch, the fan-in from level me-3 up in a second,
+    k_cascade_top) and BA_CASC_TWO=0 (the one-launch cascade) give the same bits,
+    and the oracle's; the profile shows which kernels ran."""
+    from ba_amd import lib as L
+    kw = dict(seed=0x2A + B, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1, order_mode=L.ORDER_RANDOM,
+              first_trial=64 * 9)
+    out = {}
+    for two in ("1", "0"):
+        monkeypatch.setenv("BA_CASC_TWO", two)
+        engine.profile(True)
+        out[two] = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
+        prof = engine.profile_read()
+        engine.profile(False)
+        assert ("k_cascade_top" in prof) == (two == "1"), prof
+    monkeypatch.delenv("BA_CASC_TWO")
+    a, b = out["1"], out["0"]
+    same(a.decisions, b.decisions, "decisions")
+    same(a.outcome, b.outcome, "outcome")
+    assert a.counters == b.counters
+    if B <= 700:
+        _check(a, n, m, B, **kw)
+
+
+def test_two_launch_handoff_tags(engine, monkeypatch):
+    """The two-launch mode in the check build: the fan-in launch reads every child
+    the units launch wrote with this call's epoch (60 calls, batch 1024 and 512)."""
+    monkeypatch.setenv("BA_CASC_TWO", "1")
+    monkeypatch.setenv("BA_CASC_CHECK", "1")
+    mism, cnt, _ = _check_calls(engine, 16, 5, (1024, 512), 60, 1)
+    assert int(mism.sum()) == 0
+    assert (cnt[:, 0] > 0).all()
