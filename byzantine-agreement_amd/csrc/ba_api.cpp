@@ -605,7 +605,7 @@ static bool use_cascade(ba_ctx* ctx, const Geometry& g) {
     return !off && ctx->leaf_fusion && leaf_supported(g) && g.me >= 3 && cascade_supported(g);
 }
 
-constexpr uint64_t kCascTwoWords = 8;
+constexpr uint64_t kCascTwoWords = 1;
 
 // BA_CASC_CHECK (tests only, read per call): 1 = the cascade's check build
 // (epoch tags beside every hand-off word, mismatches counted into
@@ -623,7 +623,8 @@ static int run_cascade(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge, CascJob job 
     job.check = whole ? 0u : cascade_check_mode(g);
     // Two launches (units, then the fan-in) from kCascTwoWords 64-trial words on:
     // the steps' latency-bound waves then no longer hold the slots the units use
-    // (DESIGN.md §4).  BA_CASC_TWO=0/1 (read per call) forces one or two.
+    // (faster from one word up: profiles/r04h).  BA_CASC_TWO=0/1
+    // (read per call) forces one or two.
     if (!whole && g.me >= 4) {
         const char* e = getenv("BA_CASC_TWO");
         job.two = e ? atoi(e) != 0 : (a.batch + 63) / 64 >= kCascTwoWords;

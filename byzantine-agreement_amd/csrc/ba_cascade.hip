@@ -303,21 +303,17 @@ __device__ __forceinline__ void casc_put(const CascArgs& a, uint32_t w, uint32_t
 // VIN: the children are rows of the gathered vote array a.vin (the root pass of
 // the subtree split: written by an earlier launch / RCCL, plain loads), not a
 // hand-off of this launch.
-template <int N, int ME, int q, bool CHECK, bool VIN = false>
-__device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in, uint64_t* scr,
-                                          uint32_t lane, uint32_t w, uint32_t s, uint64_t gw,
-                                          TrialCounts& tc, uint32_t& mm) {
+// The children of sigma at step q: R_{q+1}[sigma.j.r], j != r -- child
+// c = r - (r > j) of level-q slot s*K + j (sigma's child block: one padded
+// group of R_{q+1}), or the vote rows (VIN).  Issued before the relay of
+// L_q[sigma.r], so its Philox work covers their latency.
+template <int N, int ME, int q, bool CHECK, bool VIN>
+__device__ __forceinline__ void casc_kids(const CascArgs& a, uint32_t lane, uint32_t w, uint32_t s,
+                                          uint64_t (&cv)[N - 1 - q - 1], uint32_t& mm) {
     using C = Casc<N, ME>;
     constexpr int L = C::L, K = L - q;
     const bool act = lane < (uint32_t)K;
     const uint32_t r = act ? lane : 0u;
-    // L_q[sigma.r], sigma's path unranked (no tables)
-    uint32_t path[q > 0 ? q : 1], srt[q > 0 ? q : 1];
-    if constexpr (q > 0) unrank_path<L, q - 1>(s, path, srt);
-    const uint64_t lq = relay_slots<N, q, K, 64>(a, in, scr, lane, true, s, s * (uint32_t)K, path, gw);
-    // R_{q+1}[sigma.j.r], j != r: child c = r - (r > j) of level-q slot s*K + j
-    // (sigma's child block: one padded group of R_{q+1})
-    uint64_t cv[K - 1];
     static_for<0, K - 1>([&](auto jj) {
         const uint32_t j = (uint32_t)jj() + ((uint32_t)jj() >= r ? 1u : 0u);
         const uint32_t x = (s * (uint32_t)K + j) * (uint32_t)(K - 1) + r - (r > j ? 1u : 0u);
@@ -331,6 +327,28 @@ __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in,
             }
         }
     });
+}
+
+template <int N, int ME, int q, bool CHECK, bool VIN = false>
+__device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in, uint64_t* scr,
+                                          uint32_t lane, uint32_t w, uint32_t s, uint64_t gw,
+                                          TrialCounts& tc, uint32_t& mm);
+
+// Step q for sigma with its children cv already loaded: relay L_q[sigma.r],
+// majority, then store + arrive (q > 0) or roots + epilogue (q = 0).
+template <int N, int ME, int q, bool CHECK>
+__device__ __forceinline__ void casc_finish(const CascArgs& a, const uint64_t* in, uint64_t* scr,
+                                            uint32_t lane, uint32_t w, uint32_t s, uint64_t gw,
+                                            const uint64_t (&cv)[N - 1 - q - 1], TrialCounts& tc,
+                                            uint32_t& mm) {
+    using C = Casc<N, ME>;
+    constexpr int L = C::L, K = L - q;
+    const bool act = lane < (uint32_t)K;
+    const uint32_t r = act ? lane : 0u;
+    // L_q[sigma.r], sigma's path unranked (no tables)
+    uint32_t path[q > 0 ? q : 1], srt[q > 0 ? q : 1];
+    if constexpr (q > 0) unrank_path<L, q - 1>(s, path, srt);
+    const uint64_t lq = relay_slots<N, q, K, 64>(a, in, scr, lane, true, s, s * (uint32_t)K, path, gw);
     Csa<planes_c(K)> cnt;
     cnt.template add<0>(lq);
     static_for<0, K - 1>([&](auto jj) { cnt.template add<jj() + 1>(cv[jj()]); });
@@ -383,6 +401,16 @@ __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in,
         if (a.counters) sink_counters(lane, mine, w, a.W, a.counters, a.sk);
         (void)tc;
     }
+}
+
+
+template <int N, int ME, int q, bool CHECK, bool VIN>
+__device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in, uint64_t* scr,
+                                          uint32_t lane, uint32_t w, uint32_t s, uint64_t gw,
+                                          TrialCounts& tc, uint32_t& mm) {
+    uint64_t cv[N - 1 - q - 1];
+    casc_kids<N, ME, q, CHECK, VIN>(a, lane, w, s, cv, mm);
+    casc_finish<N, ME, q, CHECK>(a, in, scr, lane, w, s, gw, cv, tc, mm);
 }
 
 // One block = 4 * GPW consecutive units (their words: <= nw_max, sliced into
@@ -553,11 +581,15 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade_top(CascArgs a) {
     const uint32_t w = u / PER, sg = u - w * PER;
     uint64_t* planes = sh[wv];
     uint64_t* scr = sh[wv] + ((NIN + 1) & ~1);
-    wave_inputs<N, 1, 0>(planes, lane, w, a.seed, a.gs, a.first_trial, a.ntrials, a.faulty, a.order);
-    __builtin_amdgcn_wave_barrier();
     TrialCounts tc;
     uint32_t mm = 0;
-    casc_step<N, ME, QS, CHECK, VIN>(a, planes, scr, lane, w, sg, (a.first_trial >> 6) + w, tc, mm);
+    // the children's loads go out first; the word's input loads and slicing and
+    // the relay of L_QS then overlap their latency
+    uint64_t cv[N - 1 - QS - 1];
+    casc_kids<N, ME, QS, CHECK, VIN>(a, lane, w, sg, cv, mm);
+    wave_inputs<N, 1, 0>(planes, lane, w, a.seed, a.gs, a.first_trial, a.ntrials, a.faulty, a.order);
+    __builtin_amdgcn_wave_barrier();
+    casc_finish<N, ME, QS, CHECK>(a, planes, scr, lane, w, sg, (a.first_trial >> 6) + w, cv, tc, mm);
     if constexpr (CHECK) {
         uint32_t t = mm;
 #pragma unroll
