@@ -600,6 +600,152 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade_top(CascArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// k_cascade_wtop<N, ME, QS, VIN>: the same fan-in as k_cascade_top, one BLOCK
+// of 1024 threads per word and no hand-off at all: the block relays L_0..L_QS
+// of its word into LDS (one Philox pair per item, level by level), takes every
+// level-QS majority over children from memory (R_{QS+1} of the units launch,
+// or the gathered votes), then every lower level from LDS, block barrier in
+// between, and the roots and the quorum epilogue (ba.py:159-255) by wave 0,
+// which feeds the counter sink.  k_cascade_top's chain of three hand-offs
+// (store, drain, returning add, reload) becomes three block barriers.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kWtopThreads = 1024;
+
+template <int N, int ME, int QS>
+struct CascWtop {
+    using C = Casc<N, ME>;
+    static constexpr int L = C::L, NIN = C::NIN;
+    static constexpr uint32_t oIN = 0, oAU = (NIN + 1) & ~1;
+    static constexpr uint32_t oLV = oAU + ((2 * L + 1) & ~1);
+    static constexpr uint32_t lv_off(int k) {  // L_k of the word
+        uint32_t o = oLV;
+        for (int i = 0; i < k; ++i) o += C::sz(i);
+        return o;
+    }
+    static constexpr uint32_t rv_off(int k) {  // R_k of the word, k = 1..QS
+        uint32_t o = lv_off(QS + 1);
+        for (int i = 1; i < k; ++i) o += C::sz(i);
+        return o;
+    }
+    static constexpr uint32_t words = rv_off(QS + 1);
+};
+
+template <int N, int ME, int QS, bool VIN, bool CHECK = false>
+__global__ __launch_bounds__(kWtopThreads) void k_cascade_wtop(CascArgs a) {
+    using C = Casc<N, ME>;
+    using B = CascWtop<N, ME, QS>;
+    constexpr int L = C::L;
+    constexpr uint32_t T = kWtopThreads;
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint32_t w = blockIdx.x;
+    const uint64_t gw = (a.first_trial >> 6) + w;
+    uint64_t* planes = lds + B::oIN;
+    uint64_t* au = lds + B::oAU;
+    uint32_t mm = 0;
+    if (wv == 0) wave_inputs<N, 1, 0>(planes, lane, w, a.seed, a.gs, a.first_trial, a.ntrials, a.faulty, a.order);
+    __syncthreads();
+    // relay L_0 .. L_QS (ba.py:257-285, 42-57): level k slot x is relayed by the
+    // last general of its parent slot x / (L - k)
+    static_for<0, QS + 1>([&](auto k) {
+        constexpr uint32_t SK = C::sz(k()), NP = (SK + 1) / 2;
+        uint64_t* lv = lds + B::lv_off(k());
+        for (uint32_t p = t; p < NP; p += T) {
+            uint64_t l[2];
+            lie_pair(a.seed, k(), p, gw, l[0], l[1]);
+            static_for<0, 2>([&](auto h) {
+                const uint32_t x = 2 * p + h();
+                if (x < SK) {
+                    uint64_t par, f;
+                    if constexpr (k() == 0) {
+                        par = planes[N];  // OB: the commander's order
+                        f = planes[0];
+                    } else {
+                        const uint32_t px = x / (uint32_t)(L - k());
+                        par = lds[B::lv_off(k() - 1) + px];
+                        f = planes[a.sender[a.snd_off[k() - 1] + px]];
+                    }
+                    lv[x] = sel64(f, l[h()], par);
+                }
+            });
+        }
+        __syncthreads();
+    });
+    // majorities, level QS (children from memory) down to the roots (from LDS)
+    static_for<0, QS + 1>([&](auto i) {
+        constexpr int q = QS - i();
+        constexpr int K = L - q;
+        constexpr uint32_t SQ = C::sz(q);
+        const uint64_t* lq = lds + B::lv_off(q);
+        for (uint32_t y = t; y < SQ; y += T) {
+            const uint32_t sg = y / (uint32_t)K, r = y - sg * (uint32_t)K;
+            uint64_t cv[K - 1];
+            static_for<0, K - 1>([&](auto jj) {
+                const uint32_t j = (uint32_t)jj() + ((uint32_t)jj() >= r ? 1u : 0u);
+                const uint32_t x = (sg * (uint32_t)K + j) * (uint32_t)(K - 1) + r - (r > j ? 1u : 0u);
+                if constexpr (q < QS) {
+                    cv[jj()] = lds[B::rv_off(q + 1) + x];
+                } else if constexpr (VIN) {
+                    cv[jj()] = a.vin[(uint64_t)x * a.W + w];
+                } else {
+                    const uint64_t ix = C::template addr<q + 1>(w, x);
+                    cv[jj()] = a.R[q + 1][ix];
+                    if constexpr (CHECK) {
+                        if (a.tag[q + 1][ix] != casc_tag(a.epoch)) ++mm;
+                    }
+                }
+            });
+            Csa<planes_c(K)> cnt;
+            cnt.template add<0>(lq[y]);
+            static_for<0, K - 1>([&](auto jj) { cnt.template add<jj() + 1>(cv[jj()]); });
+            if constexpr (q > 0) {
+                lds[B::rv_off(q) + y] = cnt.template ge<K, K / 2 + 1>();  // inner tie -> non-attack
+            } else {  // roots: tie -> undefined
+                const uint64_t att = cnt.template ge<K, K / 2 + 1>();
+                au[r] = att;
+                au[L + r] = (K % 2 == 0) ? (cnt.template ge<K, K / 2>() & ~att) : 0ull;
+            }
+        }
+        __syncthreads();
+    });
+    if constexpr (CHECK) {
+        uint32_t v = mm;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (lane == 0 && v != 0 && a.counters)
+            atomicAdd((unsigned long long*)(a.counters + BA_C_CHECK_MISMATCH), (unsigned long long)v);
+    }
+    if (wv == 0) {
+        TrialCounts tw;
+        wave_epilogue<N, 1, (uint32_t)ME, 0>(planes, au, lane, w, a.ntrials, a.decisions, a.outcome, tw);
+        uint64_t mine = 0;
+#pragma unroll
+        for (int c = 0; c < C_NUM; ++c) {
+            uint32_t x = tw.v[c];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+            if (lane == (uint32_t)c) mine = x;
+        }
+        if (a.counters) sink_counters(lane, mine, w, a.W, a.counters, a.sk);
+    }
+}
+
+template <int N, int ME, int QS, bool VIN, bool CHECK = false>
+static hipError_t launch_wtop(const CascArgs& ca, uint32_t W, hipStream_t st) {
+    using B = CascWtop<N, ME, QS>;
+    hipLaunchKernelGGL((k_cascade_wtop<N, ME, QS, VIN, CHECK>), dim3(W), dim3(kWtopThreads),
+                       (size_t)B::words * sizeof(uint64_t), st, ca);
+    return hipGetLastError();
+}
+
+// BA_CASC_WTOP=0 (read per call; A/B): the fan-in by k_cascade_top (one wave
+// per level-(QS-1) slot, hand-offs) instead of one block per word
+static bool use_wtop() {
+    const char* e = getenv("BA_CASC_WTOP");
+    return !(e && e[0] == '0');
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 #define BA_CASC_SHAPES(X) X(16, 5) X(16, 4) X(16, 3) X(10, 3) X(9, 4) X(8, 5)
@@ -702,6 +848,19 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
     ca.outcome = a.outcome ? a.outcome + trial0 : nullptr;
     ca.counters = job.h ? nullptr : a.counters;
     ca.sk = a.sink;
+    if (job.vin && use_wtop()) {  // the split's root pass: one block per word
+        ca.vin = job.vin;
+        ca.h = 0;
+        ca.counters = a.counters;
+        ProfScope ps(a.prof, "k_cascade_wtop", a.stream);
+#define BA_CASC_WROOT_LAUNCH(nn, mm)                                                               \
+    if (g.n == nn && g.me == mm)                                                                  \
+        return job.root_h == 2 ? launch_wtop<nn, mm, 1, true>(ca, (uint32_t)W, a.stream)          \
+                               : launch_wtop<nn, mm, 0, true>(ca, (uint32_t)W, a.stream);
+        BA_CASC_RANGE_SHAPES(BA_CASC_WROOT_LAUNCH)
+#undef BA_CASC_WROOT_LAUNCH
+        return hipErrorInvalidValue;
+    }
     if (job.vin) {  // the split's root pass: one wave per (word, level root_h-2 slot)
         ca.vin = job.vin;
         ca.h = 0;
@@ -737,6 +896,16 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
             if (e != hipSuccess) return e;
         }
         CascArgs ct = ca;
+        if (use_wtop()) {
+            ProfScope ps(a.prof, "k_cascade_wtop", a.stream);
+#define BA_CASC_WTOP_LAUNCH(nn, mm)                                                          \
+    if (g.n == nn && g.me == mm)                                                           \
+        return job.check ? launch_wtop<nn, mm, mm - 3, false, true>(ct, (uint32_t)W, a.stream) \
+                         : launch_wtop<nn, mm, mm - 3, false>(ct, (uint32_t)W, a.stream);
+            BA_CASC_TWO_SHAPES(BA_CASC_WTOP_LAUNCH)
+#undef BA_CASC_WTOP_LAUNCH
+            return hipErrorInvalidValue;
+        }
         ct.units = (uint32_t)(W * g.S[g.me - 4]);
         ProfScope ps(a.prof, "k_cascade_top", a.stream);
         const uint32_t blocks = (ct.units + kCascWaves - 1) / kCascWaves;

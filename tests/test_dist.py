@@ -288,7 +288,7 @@ def test_subtree_votes_match_oracle_gpu(engine, monkeypatch, n, m, B, nr, nocasc
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nocasc", ["0", "1"])
+@pytest.mark.parametrize("nocasc", ["0", "1", "wave"])
 @pytest.mark.parametrize("n,m,B,nr", [(10, 3, 200, 4), (9, 4, 130, 3), (13, 4, 65, 5),
                                       (7, 3, 100, 3), (16, 5, 2, 8), (16, 5, 70, 8), (8, 5, 300, 5)])
 def test_second_hop_votes_match_oracle_gpu(engine, monkeypatch, n, m, B, nr, nocasc):
@@ -298,7 +298,8 @@ def test_second_hop_votes_match_oracle_gpu(engine, monkeypatch, n, m, B, nr, noc
     through the cascade (range-mode votes, k_cascade_root) where the shape has it,
     and through the multi-launch LEVELS kernels (BA_NO_CASCADE=1)."""
     from ba_amd import lib as L
-    monkeypatch.setenv("BA_NO_CASCADE", nocasc)
+    monkeypatch.setenv("BA_NO_CASCADE", "1" if nocasc == "1" else "0")
+    monkeypatch.setenv("BA_CASC_WTOP", "0" if nocasc == "wave" else "1")  # root pass by waves / blocks
     dev = torch.device("cuda", 0)
     kw = dict(seed=13, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1, order_mode=L.ORDER_RANDOM,
               first_trial=64 * 5)

@@ -204,7 +204,7 @@ def test_two_launch_equals_one_launch(engine, monkeypatch, n, m, B):
         out[two] = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
         prof = engine.profile_read()
         engine.profile(False)
-        assert ("k_cascade_top" in prof) == (two == "1"), prof
+        assert any(k in prof for k in ("k_cascade_top", "k_cascade_wtop")) == (two == "1"), prof
     monkeypatch.delenv("BA_CASC_TWO")
     a, b = out["1"], out["0"]
     same(a.decisions, b.decisions, "decisions")
@@ -222,3 +222,27 @@ def test_two_launch_handoff_tags(engine, monkeypatch):
     mism, cnt, _ = _check_calls(engine, 16, 5, (1024, 512), 60, 1)
     assert int(mism.sum()) == 0
     assert (cnt[:, 0] > 0).all()
+
+
+@pytest.mark.parametrize("n,m,B", [(16, 5, 1024), (16, 5, 1), (16, 4, 130), (9, 4, 700), (8, 5, 200)])
+def test_fanin_block_per_word_equals_wave_steps(engine, monkeypatch, n, m, B):
+    """The two-launch fan-in by one block per word (k_cascade_wtop, default) and by
+    one wave per level-(me-4) slot with hand-offs (BA_CASC_WTOP=0, k_cascade_top)
+    give the same bits; and the oracle's."""
+    from ba_amd import lib as L
+    kw = dict(seed=0x77 + B, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1, order_mode=L.ORDER_RANDOM,
+              first_trial=64 * 4)
+    monkeypatch.setenv("BA_CASC_TWO", "1")
+    out = {}
+    for wt in ("1", "0"):
+        monkeypatch.setenv("BA_CASC_WTOP", wt)
+        engine.profile(True)
+        out[wt] = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
+        prof = engine.profile_read()
+        engine.profile(False)
+        assert ("k_cascade_wtop" in prof) == (wt == "1") and ("k_cascade_top" in prof) == (wt == "0"), prof
+    same(out["1"].decisions, out["0"].decisions, "decisions")
+    same(out["1"].outcome, out["0"].outcome, "outcome")
+    assert out["1"].counters == out["0"].counters
+    if B <= 200:
+        _check(out["1"], n, m, B, **kw)
