@@ -738,11 +738,17 @@ static hipError_t launch_wtop(const CascArgs& ca, uint32_t W, hipStream_t st) {
     return hipGetLastError();
 }
 
-// BA_CASC_WTOP=0 (read per call; A/B): the fan-in by k_cascade_top (one wave
-// per level-(QS-1) slot, hand-offs) instead of one block per word
-static bool use_wtop() {
+// Which fan-in kernel: one block per word (k_cascade_wtop) or one wave per
+// level-(QS-1) slot with hand-offs (k_cascade_top).  Measured (profiles/r04i):
+// the split's root pass (QS <= 1, children = votes) is faster by blocks (batch
+// 1: 4.8 vs 5.1 us at h = 1, 5.5 vs 6.8 at h = 2), the two-launch cascade's
+// fan-in from level me-3 by waves (n=16 m=5: 66.0 vs 67.2 us per 1024-instance
+// call, 18.1 vs 21.2 us per instance: one block per word leaves the chip idle
+// at small batches).  BA_CASC_WTOP=1/0 (read per call; A/B) forces one.
+static bool use_wtop(bool root_pass) {
     const char* e = getenv("BA_CASC_WTOP");
-    return !(e && e[0] == '0');
+    if (e) return e[0] != '0';
+    return root_pass;
 }
 
 // ---------------------------------------------------------------------------
@@ -848,7 +854,7 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
     ca.outcome = a.outcome ? a.outcome + trial0 : nullptr;
     ca.counters = job.h ? nullptr : a.counters;
     ca.sk = a.sink;
-    if (job.vin && use_wtop()) {  // the split's root pass: one block per word
+    if (job.vin && use_wtop(true)) {  // the split's root pass: one block per word
         ca.vin = job.vin;
         ca.h = 0;
         ca.counters = a.counters;
@@ -896,7 +902,7 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
             if (e != hipSuccess) return e;
         }
         CascArgs ct = ca;
-        if (use_wtop()) {
+        if (use_wtop(false)) {
             ProfScope ps(a.prof, "k_cascade_wtop", a.stream);
 #define BA_CASC_WTOP_LAUNCH(nn, mm)                                                          \
     if (g.n == nn && g.me == mm)                                                           \

@@ -226,9 +226,9 @@ def test_two_launch_handoff_tags(engine, monkeypatch):
 
 @pytest.mark.parametrize("n,m,B", [(16, 5, 1024), (16, 5, 1), (16, 4, 130), (9, 4, 700), (8, 5, 200)])
 def test_fanin_block_per_word_equals_wave_steps(engine, monkeypatch, n, m, B):
-    """The two-launch fan-in by one block per word (k_cascade_wtop, default) and by
-    one wave per level-(me-4) slot with hand-offs (BA_CASC_WTOP=0, k_cascade_top)
-    give the same bits; and the oracle's."""
+    """The two-launch fan-in by one block per word (k_cascade_wtop, BA_CASC_WTOP=1)
+    and by one wave per level-(me-4) slot with hand-offs (BA_CASC_WTOP=0,
+    k_cascade_top, the default there) give the same bits; and the oracle's."""
     from ba_amd import lib as L
     kw = dict(seed=0x77 + B, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1, order_mode=L.ORDER_RANDOM,
               first_trial=64 * 4)
