@@ -429,8 +429,11 @@ __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in,
 // k_cascade_top does the fan-in; alone: the lab's units-only ablation), 4 =
 // arrivals but no steps (lab only, tools/casc_lab.py, BA_CASC_DIAG; wrong
 // results).  The one-launch product uses 0.
+#ifndef BA_CASC_MINB
+#define BA_CASC_MINB(n, me, diag) 1
+#endif
 template <int N, int ME, int DIAG = 0, bool CHECK = false>
-__global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
+__global__ __launch_bounds__(64 * kCascWaves, BA_CASC_MINB(N, ME, DIAG)) void k_cascade(CascArgs a) {
     using C = Casc<N, ME>;
     constexpr int L = C::L, S = C::S, G = C::G, GP = C::GP, GPW = C::GPW, NIN = C::NIN, Q = C::Q;
     constexpr int NPD = (S + 1) / 2;
