@@ -429,9 +429,12 @@ __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in,
 // k_cascade_top does the fan-in; alone: the lab's units-only ablation), 4 =
 // arrivals but no steps (lab only, tools/casc_lab.py, BA_CASC_DIAG; wrong
 // results).  The one-launch product uses 0.
-#ifndef BA_CASC_MINB
-#define BA_CASC_MINB(n, me, diag) 1
+// minimum blocks per CU of the units-only launch (DIAG 2): A/B builds set
+// -DBA_CASC_UNITS_MINB=k (k = 4: 128 VGPRs, 4 waves/SIMD, with spills)
+#ifndef BA_CASC_UNITS_MINB
+#define BA_CASC_UNITS_MINB 1
 #endif
+#define BA_CASC_MINB(n, me, diag) ((diag) == 2 ? BA_CASC_UNITS_MINB : 1)
 template <int N, int ME, int DIAG = 0, bool CHECK = false>
 __global__ __launch_bounds__(64 * kCascWaves, BA_CASC_MINB(N, ME, DIAG)) void k_cascade(CascArgs a) {
     using C = Casc<N, ME>;
