@@ -246,3 +246,43 @@ def test_fanin_block_per_word_equals_wave_steps(engine, monkeypatch, n, m, B):
     assert out["1"].counters == out["0"].counters
     if B <= 200:
         _check(out["1"], n, m, B, **kw)
+
+
+def _fuzz_cases(k=24, seed=0xF022):
+    rng = np.random.default_rng(seed)
+    shapes = SHAPES
+    out = []
+    for i in range(k):
+        n, m = shapes[rng.integers(len(shapes))]
+        B = int(rng.choice([1, 63, 64, 65, int(rng.integers(2, 900))]))
+        mode = int(rng.integers(3))  # 0 random faulty sets, 1 exact f, 2 given inputs
+        two = str(rng.integers(2))
+        wtop = str(rng.integers(2))
+        out.append((i, n, m, B, mode, two, wtop, int(rng.integers(0, 50)), int(rng.integers(1 << 30))))
+    return out
+
+
+@pytest.mark.parametrize("i,n,m,B,mode,two,wtop,ft,sd", _fuzz_cases())
+def test_cascade_fuzz_vs_oracle(engine, monkeypatch, i, n, m, B, mode, two, wtop, ft, sd):
+    """Seeded random cascade calls: every shape k_cascade is compiled for, batch 1 to
+    900 (ragged, one word, word edges), random / exact-f / given faulty sets and
+    orders (incl. non-attack/retreat), random first_trial and seed, one- or two-launch
+    (BA_CASC_TWO), fan-in by waves or by blocks (BA_CASC_WTOP): bit-exact with the
+    oracle on decisions, outcome bytes and counters."""
+    from ba_amd import lib as L
+    monkeypatch.setenv("BA_CASC_TWO", two)
+    monkeypatch.setenv("BA_CASC_WTOP", wtop)
+    if mode == 2:
+        rng = np.random.default_rng(sd)
+        fm = (rng.integers(0, 1 << n, B, dtype=np.uint64) & rng.integers(0, 1 << n, B, dtype=np.uint64)
+              ).astype(np.uint32)
+        oc = rng.integers(0, 3, B).astype(np.uint8)
+        kw = dict(seed=sd, faulty=fm, order=oc, first_trial=64 * ft)
+    else:
+        kw = dict(seed=sd, faulty_mode=L.FAULTY_RANDOM if mode == 0 else L.FAULTY_EXACT,
+                  f=(n - 1) // 3 + (sd % 2), order_mode=L.ORDER_RANDOM, first_trial=64 * ft)
+    res = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
+    od, oo, oc_ = oracle_c.run(n, m, B, **kw) if B <= 128 or n < 16 else oracle_c.sliced_run(n, m, B, **kw)
+    same(res.decisions, od, f"decisions case {i}")
+    same(res.outcome, oo, f"outcome case {i}")
+    assert {k: res.counters[k] for k in oc_} == oc_, i
