@@ -32,7 +32,9 @@ for s in $STAGES; do
     tests) run pytest_gpu 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) run bench 600 python -u bench.py --steps 20 --warmup 3 || exit $? ;;
-    bench2) run bench2 600 env BA_BENCH_DEVICE=0 python -u bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu || exit $? ;;
+    bench2) run bench2 600 env BA_BENCH_DEVICE=0 python -u bench.py --gpus 2 --steps 20 --warmup 3 --cpu-budget-s 4 || exit $? ;;
+    benchreps) for r in 1 2 3; do run bench_rep$r 300 python -u bench.py --steps 20 --warmup 5 --no-cpu || exit $?; done ;;
+    configs2) run configs_l2 600 python -u tools/run_configs.py --only 5 --split-level 2 || exit $? ;;
     bench_levels) run bench_levels 600 python -u bench.py --steps 20 --warmup 3 --engine levels --no-cpu || exit $? ;;
     bench_fused) run bench_fused 600 python -u bench.py --steps 20 --warmup 3 --engine fused --no-cpu || exit $? ;;
     philox) run philox 120 ./tools/philox_bench || exit $? ;;
