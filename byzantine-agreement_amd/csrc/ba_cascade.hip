@@ -606,6 +606,86 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade_top(CascArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// k_cascade_mtop<N, ME>: the two-launch fan-in with one hand-off fewer.  One
+// block per (word, level-(Q-2) slot s0; Q = me-3 = the units' level; Q = 1: the
+// word): step Q for EVERY child sigma of s0 at once -- one group of K = L-Q
+// lanes per sigma, GW groups per wave, children R_{Q+1} from the units launch,
+// each group drawing its own relay (relay_draw over the group's K lanes) -- into
+// LDS, one block barrier, then step Q-1 for s0 by wave 0 with its children
+// from LDS (casc_finish: relay, majority, then R_{Q-1} stored + the arrival at
+// the root counter, the last arriver taking the roots, or at Q = 1 the roots
+// and the epilogue directly).  k_cascade_top hands step Q's results to step
+// Q-1 through memory (store, drain, returning add, reload); here that hop is
+// one barrier.
+// ---------------------------------------------------------------------------
+template <int N, int ME>
+struct CascMtop {
+    using C = Casc<N, ME>;
+    static constexpr int L = C::L, Q = C::Q, K = L - Q;  // step Q: K receivers per sigma
+    static constexpr int NG = L - (Q - 1);                // sigmas per block (children of s0)
+    static constexpr int GW = 64 / K;                     // sigma groups per wave
+    static constexpr int NWV = (NG + GW - 1) / GW;        // waves per block
+    static constexpr uint32_t PB = Q >= 2 ? C::sz(Q - 2) : 1u;  // blocks per word
+    static constexpr int XW = 2 * RelayPlan<N, (Q >= 1 ? Q : 1), K>::CALLS;  // relay words per group
+};
+
+template <int N, int ME, bool CHECK = false>
+__global__ __launch_bounds__(64 * kCascWaves) void k_cascade_mtop(CascArgs a) {
+    using C = Casc<N, ME>;
+    using M = CascMtop<N, ME>;
+    constexpr int L = M::L, Q = M::Q, K = M::K, NG = M::NG, GW = M::GW, NIN = C::NIN;
+    static_assert(Q >= 1 && M::NWV <= (int)kCascWaves, "k_cascade_mtop: me >= 4, <= 4 waves");
+    __shared__ __attribute__((aligned(16))) uint64_t planes[(NIN + 1) & ~1];
+    __shared__ __attribute__((aligned(16))) uint64_t xch[M::NWV * GW * M::XW];
+    __shared__ __attribute__((aligned(16))) uint64_t rv[NG * K];  // R_Q of s0's sigmas
+    __shared__ __attribute__((aligned(16))) uint64_t scr[64];      // wave 0's step Q-1 (and roots)
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t w = blockIdx.x / M::PB, s0 = blockIdx.x - w * M::PB;
+    const uint64_t gw = (a.first_trial >> 6) + w;
+    const uint32_t g = lane / (uint32_t)K, r = lane - g * (uint32_t)K;
+    const uint32_t j = wv * (uint32_t)GW + g;  // sigma = child j of s0
+    const bool act = g < (uint32_t)GW && j < (uint32_t)NG;
+    const uint32_t sg = s0 * (uint32_t)NG + (act ? j : 0u);
+    TrialCounts tc;
+    uint32_t mm = 0;
+    // children first; the inputs (wave 0) and the relay draws overlap them
+    uint64_t cv[K - 1];
+    casc_kids<N, ME, Q, CHECK, false>(a, act ? r : (uint32_t)K, w, sg, cv, mm);
+    const RelayPlan<N, Q, K> rp(sg, sg * (uint32_t)K);
+    uint64_t* xg = xch + (wv * (uint32_t)GW + (act ? g : 0u)) * (uint32_t)M::XW;
+    relay_draw<N, Q, K, K>(a, rp, xg, r, act, gw);
+    if (wv == 0) wave_inputs<N, 1, 0>(planes, lane, w, a.seed, a.gs, a.first_trial, a.ntrials, a.faulty, a.order);
+    __syncthreads();
+    if (act) {
+        uint32_t path[Q], srt[Q];
+        unrank_path<L, Q - 1>(sg, path, srt);
+        const uint64_t lq = relay_apply<N, Q, K>(rp, planes, xg, r, sg * (uint32_t)K, path);
+        Csa<planes_c(K)> cnt;
+        cnt.template add<0>(lq);
+        static_for<0, K - 1>([&](auto jj) { cnt.template add<jj() + 1>(cv[jj()]); });
+        rv[j * (uint32_t)K + r] = cnt.template ge<K, K / 2 + 1>();  // inner tie -> non-attack
+    }
+    __syncthreads();
+    if (wv == 0) {
+        // step Q-1 for s0: receiver r1 = lane < NG, children R_Q[s0.j1.r1], j1 != r1
+        const uint32_t r1 = lane < (uint32_t)NG ? lane : 0u;
+        uint64_t cv1[NG - 1];
+        static_for<0, NG - 1>([&](auto jj) {
+            const uint32_t j1 = (uint32_t)jj() + ((uint32_t)jj() >= r1 ? 1u : 0u);
+            cv1[jj()] = rv[j1 * (uint32_t)K + r1 - (r1 > j1 ? 1u : 0u)];
+        });
+        casc_finish<N, ME, Q - 1, CHECK>(a, planes, scr, lane, w, s0, gw, cv1, tc, mm);
+    }
+    if constexpr (CHECK) {
+        uint32_t t = mm;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+        if (lane == 0 && t != 0 && a.counters)
+            atomicAdd((unsigned long long*)(a.counters + BA_C_CHECK_MISMATCH), (unsigned long long)t);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_cascade_wtop<N, ME, QS, VIN>: the same fan-in as k_cascade_top, one BLOCK
 // of 1024 threads per word and no hand-off at all: the block relays L_0..L_QS
 // of its word into LDS (one Philox pair per item, level by level), takes every
@@ -755,6 +835,13 @@ static bool use_wtop(bool root_pass) {
     const char* e = getenv("BA_CASC_WTOP");
     if (e) return e[0] != '0';
     return root_pass;
+}
+// The two-launch fan-in by k_cascade_mtop (one hand-off fewer) or k_cascade_top.
+// BA_CASC_MTOP=1/0 (read per call; A/B) forces one.
+static bool use_mtop() {
+    const char* e = getenv("BA_CASC_MTOP");
+    if (e) return e[0] != '0';
+    return true;
 }
 
 // ---------------------------------------------------------------------------
@@ -916,6 +1003,22 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
                          : launch_wtop<nn, mm, mm - 3, false>(ct, (uint32_t)W, a.stream);
             BA_CASC_TWO_SHAPES(BA_CASC_WTOP_LAUNCH)
 #undef BA_CASC_WTOP_LAUNCH
+            return hipErrorInvalidValue;
+        }
+        if (use_mtop()) {
+            ProfScope ps(a.prof, "k_cascade_mtop", a.stream);
+#define BA_CASC_MTOP_LAUNCH(nn, mm)                                                                   \
+    if (g.n == nn && g.me == mm) {                                                                  \
+        using M = CascMtop<nn, mm>;                                                                 \
+        const dim3 grid((uint32_t)(W * M::PB)), blk(64 * M::NWV);                                    \
+        if (job.check)                                                                              \
+            hipLaunchKernelGGL((k_cascade_mtop<nn, mm, true>), grid, blk, 0, a.stream, ct);          \
+        else                                                                                        \
+            hipLaunchKernelGGL((k_cascade_mtop<nn, mm>), grid, blk, 0, a.stream, ct);                \
+        return hipGetLastError();                                                                   \
+    }
+            BA_CASC_TWO_SHAPES(BA_CASC_MTOP_LAUNCH)
+#undef BA_CASC_MTOP_LAUNCH
             return hipErrorInvalidValue;
         }
         ct.units = (uint32_t)(W * g.S[g.me - 4]);

@@ -204,7 +204,7 @@ def test_two_launch_equals_one_launch(engine, monkeypatch, n, m, B):
         out[two] = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
         prof = engine.profile_read()
         engine.profile(False)
-        assert any(k in prof for k in ("k_cascade_top", "k_cascade_wtop")) == (two == "1"), prof
+        assert any(k in prof for k in ("k_cascade_top", "k_cascade_wtop", "k_cascade_mtop")) == (two == "1"), prof
     monkeypatch.delenv("BA_CASC_TWO")
     a, b = out["1"], out["0"]
     same(a.decisions, b.decisions, "decisions")
@@ -214,38 +214,49 @@ def test_two_launch_equals_one_launch(engine, monkeypatch, n, m, B):
         _check(a, n, m, B, **kw)
 
 
-def test_two_launch_handoff_tags(engine, monkeypatch):
+@pytest.mark.parametrize("mtop", ["1", "0"])
+def test_two_launch_handoff_tags(engine, monkeypatch, mtop):
     """The two-launch mode in the check build: the fan-in launch reads every child
-    the units launch wrote with this call's epoch (60 calls, batch 1024 and 512)."""
+    the units launch wrote with this call's epoch (60 calls, batch 1024 and 512),
+    fan-in by k_cascade_mtop and by k_cascade_top."""
     monkeypatch.setenv("BA_CASC_TWO", "1")
+    monkeypatch.setenv("BA_CASC_MTOP", mtop)
     monkeypatch.setenv("BA_CASC_CHECK", "1")
     mism, cnt, _ = _check_calls(engine, 16, 5, (1024, 512), 60, 1)
     assert int(mism.sum()) == 0
     assert (cnt[:, 0] > 0).all()
 
 
+FANIN = {"wtop": {"BA_CASC_WTOP": "1", "BA_CASC_MTOP": "0"},
+         "top": {"BA_CASC_WTOP": "0", "BA_CASC_MTOP": "0"},
+         "mtop": {"BA_CASC_WTOP": "0", "BA_CASC_MTOP": "1"}}
+
+
 @pytest.mark.parametrize("n,m,B", [(16, 5, 1024), (16, 5, 1), (16, 4, 130), (9, 4, 700), (8, 5, 200)])
-def test_fanin_block_per_word_equals_wave_steps(engine, monkeypatch, n, m, B):
-    """The two-launch fan-in by one block per word (k_cascade_wtop, BA_CASC_WTOP=1)
-    and by one wave per level-(me-4) slot with hand-offs (BA_CASC_WTOP=0,
-    k_cascade_top, the default there) give the same bits; and the oracle's."""
+def test_fanin_variants_agree(engine, monkeypatch, n, m, B):
+    """The two-launch fan-in three ways -- one block per word (k_cascade_wtop), one
+    wave per level-(me-4) slot with hand-offs (k_cascade_top), one block per
+    level-(me-5) slot with one hand-off fewer (k_cascade_mtop, the default) --
+    gives the same bits; and the oracle's."""
     from ba_amd import lib as L
     kw = dict(seed=0x77 + B, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1, order_mode=L.ORDER_RANDOM,
               first_trial=64 * 4)
     monkeypatch.setenv("BA_CASC_TWO", "1")
     out = {}
-    for wt in ("1", "0"):
-        monkeypatch.setenv("BA_CASC_WTOP", wt)
+    for name, env in FANIN.items():
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         engine.profile(True)
-        out[wt] = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
+        out[name] = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
         prof = engine.profile_read()
         engine.profile(False)
-        assert ("k_cascade_wtop" in prof) == (wt == "1") and ("k_cascade_top" in prof) == (wt == "0"), prof
-    same(out["1"].decisions, out["0"].decisions, "decisions")
-    same(out["1"].outcome, out["0"].outcome, "outcome")
-    assert out["1"].counters == out["0"].counters
+        assert {x for x in FANIN if f"k_cascade_{x}" in prof} == {name}, prof
+    for name in ("top", "mtop"):
+        same(out["wtop"].decisions, out[name].decisions, f"decisions {name}")
+        same(out["wtop"].outcome, out[name].outcome, f"outcome {name}")
+        assert out["wtop"].counters == out[name].counters, name
     if B <= 200:
-        _check(out["1"], n, m, B, **kw)
+        _check(out["mtop"], n, m, B, **kw)
 
 
 def _fuzz_cases(k=24, seed=0xF022):
@@ -257,21 +268,22 @@ def _fuzz_cases(k=24, seed=0xF022):
         B = int(rng.choice([1, 63, 64, 65, int(rng.integers(2, 900))]))
         mode = int(rng.integers(3))  # 0 random faulty sets, 1 exact f, 2 given inputs
         two = str(rng.integers(2))
-        wtop = str(rng.integers(2))
-        out.append((i, n, m, B, mode, two, wtop, int(rng.integers(0, 50)), int(rng.integers(1 << 30))))
+        fanin = list(FANIN)[int(rng.integers(len(FANIN)))]
+        out.append((i, n, m, B, mode, two, fanin, int(rng.integers(0, 50)), int(rng.integers(1 << 30))))
     return out
 
 
-@pytest.mark.parametrize("i,n,m,B,mode,two,wtop,ft,sd", _fuzz_cases())
-def test_cascade_fuzz_vs_oracle(engine, monkeypatch, i, n, m, B, mode, two, wtop, ft, sd):
+@pytest.mark.parametrize("i,n,m,B,mode,two,fanin,ft,sd", _fuzz_cases())
+def test_cascade_fuzz_vs_oracle(engine, monkeypatch, i, n, m, B, mode, two, fanin, ft, sd):
     """Seeded random cascade calls: every shape k_cascade is compiled for, batch 1 to
     900 (ragged, one word, word edges), random / exact-f / given faulty sets and
     orders (incl. non-attack/retreat), random first_trial and seed, one- or two-launch
-    (BA_CASC_TWO), fan-in by waves or by blocks (BA_CASC_WTOP): bit-exact with the
+    (BA_CASC_TWO), the two-launch fan-in by any of the three kernels: bit-exact with the
     oracle on decisions, outcome bytes and counters."""
     from ba_amd import lib as L
     monkeypatch.setenv("BA_CASC_TWO", two)
-    monkeypatch.setenv("BA_CASC_WTOP", wtop)
+    for k, v in FANIN[fanin].items():
+        monkeypatch.setenv(k, v)
     if mode == 2:
         rng = np.random.default_rng(sd)
         fm = (rng.integers(0, 1 << n, B, dtype=np.uint64) & rng.integers(0, 1 << n, B, dtype=np.uint64)

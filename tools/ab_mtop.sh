@@ -1,0 +1,9 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_cascade.py > gpurun_out/casc.log 2>&1 || { tail -30 gpurun_out/casc.log; exit 1; }
+tail -2 gpurun_out/casc.log
+for rep in 1 2; do for mt in 1 0; do for b in 1024 1; do
+  echo "mtop=$mt batch=$b rep=$rep" >> gpurun_out/ab.log
+  BA_CASC_MTOP=$mt timeout -k 10 120 python tools/config5_prof.py --batch $b --reps 300 >> gpurun_out/ab.log 2>&1 || exit 1
+done; done; done
+grep -E "mtop|us_per_call" gpurun_out/ab.log | sed -E 's/.*"us_per_call": ([0-9.]+).*/  \1 us/'
