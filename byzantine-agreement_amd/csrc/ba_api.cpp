@@ -625,7 +625,9 @@ static int run_cascade(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge, CascJob job 
     // the steps' latency-bound waves then no longer hold the slots the units use
     // (faster from one word up: profiles/r04h).  BA_CASC_TWO=0/1
     // (read per call) forces one or two.
-    if (!whole && g.me >= 4) {
+    // The subtree split's range mode too (units, then k_cascade_mtop ending at the
+    // vote level), where the shape has it.
+    if (!job.vin && g.me >= 4 && (job.h == 0 || cascade_range_two_supported(g, job.h))) {
         const char* e = getenv("BA_CASC_TWO");
         job.two = e ? atoi(e) != 0 : (a.batch + 63) / 64 >= kCascTwoWords;
     }

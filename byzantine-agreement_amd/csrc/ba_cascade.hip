@@ -88,6 +88,8 @@ struct CascArgs {
                                        // cnt_off[Q]: the word's root counter at cnt_off[Q] + w
     uint32_t h;           // range mode: the vote level (1 or 2); 0 = whole tree
     uint32_t ub;          // range mode: first h-hop subtree of the range
+    uint32_t ue;          // range mode: one past the last
+    uint32_t s0b, s0n;    // k_cascade_mtop: its level-(me-5) slots per word, [s0b, s0b + s0n)
     uint64_t* votes;      // range mode: [(u - ub)(L - h) + c][W]
     const uint64_t* vin;  // root mode: every unit's votes, [level-h slot][W]
     uint64_t* decisions;  // chunk-relative
@@ -131,6 +133,17 @@ struct Casc {
     static constexpr uint32_t planes_words = (nw_max * NIN + 1u) & ~1u;
 };
 
+// The units' lane layout: one lane per level-(me-2) slot, or two (LAT: latency
+// mode, leaf_half), G slots per unit, GPW units per wave.
+template <int N, int ME, bool LAT>
+struct CascU {
+    using C = Casc<N, ME>;
+    static constexpr int LPS = LAT ? 2 : 1, GL = C::G * LPS, GPW = 64 / GL;
+    static constexpr int tr_words = GPW * C::G * C::GP;
+    static constexpr uint32_t nw_max = (kCascWaves * GPW + C::rr_min - 1) / C::rr_min + 1;
+    static constexpr uint32_t planes_words = (nw_max * C::NIN + 1u) & ~1u;
+};
+
 // CHECK: the tag stored beside every R word of one launch
 __device__ __forceinline__ uint64_t casc_tag(uint64_t epoch) { return epoch | (~epoch << 32); }
 
@@ -141,6 +154,133 @@ __device__ __forceinline__ uint64_t lie_word(uint64_t seed, uint32_t k, uint32_t
     uint64_t l0, l1;
     lie_pair(seed, k, x >> 1, gw, l0, l1);
     return (x & 1u) ? l1 : l0;
+}
+
+// ---------------------------------------------------------------------------
+// Latency mode: one leaf block on TWO lanes (lanes 2x, 2x+1 of a unit), for
+// batches too small to fill the chip, where a lane's chain of S(S-1)/2 Philox
+// calls in a row is the units' time.  Lane h = 1 works in MIRRORED labels:
+// member a is its member S-1-a.  Mirroring maps slot e = a(S-1) + c of the
+// block to E-1-e (E = S(S-1)), so Philox pair q to NPAIR-1-q with the two
+// halves swapped, and receiver b to S-1-b.  Both lanes then run ONE compile-time
+// schedule in their own labels (SIMD code cannot branch per lane): rows
+// 0..M-1 (M = (S-1)/2) whole, row M's first floor(NPR/2) pairs (NPR = pairs
+// per row), and for odd NPR row M's middle pair, whose first local half only
+// each lane counts (lane 0: actual receiver M-1, lane 1: M+1).  Lane 0 covers
+// actual rows 0..M-1, lane 1 rows S-1..M+1, row M is shared: every pair once,
+// the middle pair on both lanes (one call of S(S-1)/2 extra per lane pair).
+// Counts are partial per receiver; each lane adds its partner's count of the
+// same actual receiver (its own index S-1-b, one DPP swap per word) and takes
+// the majority: RL[b] = R of local receiver b, on both lanes.  S odd only.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t swap_pair64(uint64_t v) {
+    return (uint64_t)swap_pair((uint32_t)(v >> 32)) << 32 | swap_pair((uint32_t)v);
+}
+
+struct LeafHalf {
+    // step k of a lane's schedule -> local (row i, pair cp); half 1 used unless mid
+    static constexpr int rows(int S) { return (S - 1) / 2; }
+    static constexpr int npr(int S) { return (S - 1) / 2; }
+    static constexpr int steps(int S) {
+        return rows(S) * npr(S) + npr(S) / 2 + (npr(S) % 2 == 1 ? 1 : 0);
+    }
+    static constexpr int row(int S, int k) {
+        return k < rows(S) * npr(S) ? k / npr(S) : rows(S);
+    }
+    static constexpr int cp(int S, int k) {
+        return k < rows(S) * npr(S) ? k % npr(S) : k - rows(S) * npr(S);
+    }
+    static constexpr bool mid(int S, int k) { return npr(S) % 2 == 1 && k == steps(S) - 1; }
+    static constexpr int recv(int S, int k, int h) {
+        const int c = 2 * cp(S, k) + h, i = row(S, k);
+        return c + (c >= i ? 1 : 0);
+    }
+    // adds receiver b's counter holds before step k half h (slot 0: its diag)
+    static constexpr int before(int S, int b, int k, int h) {
+        int n = 1;
+        for (int u = 0; u <= k; ++u)
+            for (int hh = 0; hh < 2; ++hh) {
+                if (u == k && hh >= h) return n;
+                if (hh == 1 && mid(S, u)) continue;
+                if (recv(S, u, hh) == b) ++n;
+            }
+        return n;
+    }
+    static constexpr int total(int S, int b) { return before(S, b, steps(S), 0); }
+    static constexpr int max_total(int S) {
+        int m = 0;
+        for (int b = 0; b < S; ++b) m = total(S, b) > m ? total(S, b) : m;
+        return m;
+    }
+};
+
+template <int NB>
+__device__ __forceinline__ uint64_t ge_bits(const uint64_t (&s)[NB], int th) {
+    // s (binary digits) >= th, MSB first
+    uint64_t gt = 0, eq = ~0ull;
+#pragma unroll
+    for (int i = NB - 1; i >= 0; --i) {
+        if ((th >> i) & 1) {
+            eq &= s[i];
+        } else {
+            gt |= eq & s[i];
+            eq &= ~s[i];
+        }
+    }
+    return gt | eq;
+}
+
+template <int S>
+__device__ __forceinline__ void leaf_half(uint32_t me, uint64_t seed, uint64_t gw, uint32_t sr, uint32_t h,
+                                          const uint64_t (&diagL)[S], const uint64_t (&FmL)[S],
+                                          uint64_t (&RL)[S]) {
+    static_assert(S % 2 == 1 && S >= 3, "leaf_half: odd S");
+    using LH = LeafHalf;
+    constexpr int NPAIR = S * (S - 1) / 2, NST = LH::steps(S);
+    constexpr int NL = planes_c(LH::max_total(S));
+    constexpr int PG = NST % 4 == 0 ? 4 : (NST % 3 == 0 ? 3 : 4);
+    Csa<NL> cnt[S];
+    const uint64_t dmask = h ? 0ull : ~0ull;  // each receiver's own value: lane 0 counts it
+    static_for<0, S>([&](auto b) { cnt[b()].template add<0>(diagL[b()] & dmask); });
+    const uint32_t base = sr * (uint32_t)NPAIR + (h ? (uint32_t)(NPAIR - 1) : 0u);
+    static_for<0, (NST + PG - 1) / PG>([&](auto grp) {
+        constexpr int k0 = grp() * PG, ng = NST - k0 < PG ? NST - k0 : PG;
+        P4 c[ng];
+        static_for<0, ng>([&](auto g) {
+            constexpr uint32_t kp = (uint32_t)(LH::row(S, k0 + g()) * ((S - 1) / 2) + LH::cp(S, k0 + g()));
+            uint32_t cx = h ? base - kp : base + kp;
+            asm("" : "+v"(cx));
+            c[g()] = P4{cx, me, (uint32_t)gw, (uint32_t)(gw >> 32)};
+        });
+        philox10_n<ng>(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+        static_for<0, ng>([&](auto g) {
+            constexpr int k = k0 + g(), i = LH::row(S, k);
+            const uint64_t w0 = (uint64_t)c[g()].y << 32 | c[g()].x, w1 = (uint64_t)c[g()].w << 32 | c[g()].z;
+            static_for<0, 2>([&](auto hh) {
+                if constexpr (!(hh() == 1 && LH::mid(S, k))) {
+                    constexpr int b = LH::recv(S, k, hh());
+                    constexpr int K = LH::before(S, b, k, hh());
+                    const uint64_t lw = (hh() == 0) == (h == 0) ? w0 : w1;  // lane 1: halves swapped
+                    cnt[b].template add<K>((FmL[i] & lw) | (~FmL[i] & diagL[i]));
+                }
+            });
+        });
+    });
+    // full counts: mine of local b plus the partner's of the same actual receiver
+    static_for<0, S>([&](auto b) {
+        constexpr int KM = LH::total(S, b()), KP = LH::total(S, S - 1 - b());
+        uint64_t rm[NL], rp[NL], s[NL + 1];
+        cnt[b()].template resolve<0, KM, false>(rm, 0);
+        cnt[S - 1 - b()].template resolve<0, KP, false>(rp, 0);
+        uint64_t cy = 0;
+        static_for<0, NL>([&](auto l) {
+            const uint64_t p = swap_pair64(rp[l()]);
+            s[l()] = rm[l()] ^ p ^ cy;
+            cy = (rm[l()] & p) | (cy & (rm[l()] ^ p));
+        });
+        s[NL] = cy;
+        RL[b()] = ge_bits<NL + 1>(s, S / 2 + 1);  // S inputs, strict majority
+    });
 }
 
 // L_K[x] (level-K slot x) of the word whose planes are `in`: the relay chain
@@ -435,10 +575,13 @@ __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in,
 #define BA_CASC_UNITS_MINB 1
 #endif
 #define BA_CASC_MINB(n, me, diag) ((diag) == 2 ? BA_CASC_UNITS_MINB : 1)
-template <int N, int ME, int DIAG = 0, bool CHECK = false>
+template <int N, int ME, int DIAG = 0, bool CHECK = false, bool LAT = false>
 __global__ __launch_bounds__(64 * kCascWaves, BA_CASC_MINB(N, ME, DIAG)) void k_cascade(CascArgs a) {
     using C = Casc<N, ME>;
-    constexpr int L = C::L, S = C::S, G = C::G, GP = C::GP, GPW = C::GPW, NIN = C::NIN, Q = C::Q;
+    using U = CascU<N, ME, LAT>;
+    constexpr int L = C::L, S = C::S, G = C::G, GP = C::GP, GPW = U::GPW, NIN = C::NIN, Q = C::Q;
+    constexpr int GL = U::GL;
+    static_assert(!LAT || (DIAG & 2) != 0, "latency mode: units-only launches");
     constexpr int NPD = (S + 1) / 2;
     constexpr uint32_t fan = (uint32_t)(L - Q);  // children of a level Q-1 slot (or of the root)
     using RP = RelayPlan<N, Q + 1, G>;
@@ -448,11 +591,12 @@ __global__ __launch_bounds__(64 * kCascWaves, BA_CASC_MINB(N, ME, DIAG)) void k_
     const uint32_t u0 = blockIdx.x * kCascWaves * GPW;
     const uint32_t wfirst = u0 / RR, nw = (min(u0 + kCascWaves * GPW, a.units) - 1u) / RR - wfirst + 1u;
     uint64_t* planes = lds;  // [nw][NIN]
-    uint64_t* tr = lds + C::planes_words + wv * (uint32_t)C::tr_words;
+    uint64_t* tr = lds + U::planes_words + wv * (uint32_t)U::tr_words;
     const uint64_t gw0 = a.first_trial >> 6;
     TrialCounts tc;
     uint32_t mm = 0;  // CHECK: stale child tags seen by this lane
-    const uint32_t g = lane / G, x = lane - g * G;
+    const uint32_t g = lane / GL, y = lane - g * GL;  // y: the lane within its unit
+    const uint32_t x = LAT ? y >> 1 : y, hh = LAT ? (y & 1u) : 0u;  // slot, half (LAT)
     const uint32_t u = u0 + wv * GPW + g;
     const bool act = g < (uint32_t)GPW && u < a.units;
     const uint32_t uu = act ? u : u0;
@@ -477,7 +621,7 @@ __global__ __launch_bounds__(64 * kCascWaves, BA_CASC_MINB(N, ME, DIAG)) void k_
     if (act) {
         mem = a.members[sr];
         lie_pairs<NPD>(a.seed, ME - 1, (sr * (uint32_t)S) >> 1, gw, lw);
-        relay_draw<N, Q + 1, G, G>(a, rp, xch, x, true, gw);
+        relay_draw<N, Q + 1, G, GL>(a, rp, xch, y, true, gw);
     }
     // 2. inputs
     if (staged) {
@@ -507,15 +651,28 @@ __global__ __launch_bounds__(64 * kCascWaves, BA_CASC_MINB(N, ME, DIAG)) void k_
             if constexpr (S % 2 == 1) lie = lw[b()] ^ ((lw[b()] ^ lw[b() + 1]) & oddmask);
             else lie = lw[b()];
             diag[b()] = sel64(fs, lie, par);
-            Fm[b()] = in[(mem >> (5 * b())) & 31u];
+            if constexpr (LAT) {  // lane 1: mirrored member labels
+                const uint32_t sh = hh ? 5u * (uint32_t)(S - 1 - b()) : 5u * (uint32_t)b();
+                Fm[b()] = in[(mem >> sh) & 31u];
+            } else {
+                Fm[b()] = in[(mem >> (5 * b())) & 31u];
+            }
         });
-        leaf_block<S>(ME, a.seed, gw, sr, diag, Fm, Rm);
-        uint64_t* t = tr + (gg * G) * GP + x;
-        t[x * GP] = par;
-        static_for<0, S>([&](auto d) { t[(d() + (d() >= x ? 1u : 0u)) * GP] = Rm[d()]; });
+        if constexpr (LAT) {
+            uint64_t diagL[S];
+            static_for<0, S>([&](auto b) { diagL[b()] = hh ? diag[S - 1 - b()] : diag[b()]; });
+            leaf_half<S>(ME, a.seed, gw, sr, hh, diagL, Fm, Rm);  // lane 0: actual labels
+        } else {
+            leaf_block<S>(ME, a.seed, gw, sr, diag, Fm, Rm);
+        }
+        if (hh == 0) {
+            uint64_t* t = tr + (gg * G) * GP + x;
+            t[x * GP] = par;
+            static_for<0, S>([&](auto d) { t[(d() + (d() >= x ? 1u : 0u)) * GP] = Rm[d()]; });
+        }
     }
     __builtin_amdgcn_wave_barrier();
-    if (act) {
+    if (act && hh == 0) {
         const uint64_t* col = tr + (gg * G + x) * GP;
         Csa<planes_c(G)> cnt;
         static_for<0, G>([&](auto b) { cnt.template add<b()>(col[b()]); });
@@ -640,12 +797,14 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade_mtop(CascArgs a) {
     __shared__ __attribute__((aligned(16))) uint64_t rv[NG * K];  // R_Q of s0's sigmas
     __shared__ __attribute__((aligned(16))) uint64_t scr[64];      // wave 0's step Q-1 (and roots)
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t w = blockIdx.x / M::PB, s0 = blockIdx.x - w * M::PB;
+    const uint32_t w = blockIdx.x / a.s0n, s0 = a.s0b + (blockIdx.x - w * a.s0n);
     const uint64_t gw = (a.first_trial >> 6) + w;
     const uint32_t g = lane / (uint32_t)K, r = lane - g * (uint32_t)K;
     const uint32_t j = wv * (uint32_t)GW + g;  // sigma = child j of s0
-    const bool act = g < (uint32_t)GW && j < (uint32_t)NG;
-    const uint32_t sg = s0 * (uint32_t)NG + (act ? j : 0u);
+    const uint32_t sg0 = s0 * (uint32_t)NG + j;
+    // range mode at the vote level h = Q: only the range's sigmas
+    const bool act = g < (uint32_t)GW && j < (uint32_t)NG && (a.h != (uint32_t)Q || (sg0 >= a.ub && sg0 < a.ue));
+    const uint32_t sg = act ? sg0 : s0 * (uint32_t)NG;
     TrialCounts tc;
     uint32_t mm = 0;
     // children first; the inputs (wave 0) and the relay draws overlap them
@@ -663,8 +822,11 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade_mtop(CascArgs a) {
         Csa<planes_c(K)> cnt;
         cnt.template add<0>(lq);
         static_for<0, K - 1>([&](auto jj) { cnt.template add<jj() + 1>(cv[jj()]); });
-        rv[j * (uint32_t)K + r] = cnt.template ge<K, K / 2 + 1>();  // inner tie -> non-attack
+        const uint64_t rq = cnt.template ge<K, K / 2 + 1>();  // inner tie -> non-attack
+        if (a.h == (uint32_t)Q) a.votes[((uint64_t)(sg - a.ub) * K + r) * a.W + w] = rq;  // range: votes
+        else rv[j * (uint32_t)K + r] = rq;
     }
+    if (a.h == (uint32_t)Q) return;  // block-uniform: the range's fan-in ends at these votes
     __syncthreads();
     if (wv == 0) {
         // step Q-1 for s0: receiver r1 = lane < NG, children R_Q[s0.j1.r1], j1 != r1
@@ -836,6 +998,22 @@ static bool use_wtop(bool root_pass) {
     if (e) return e[0] != '0';
     return root_pass;
 }
+// The units launch in latency mode (two lanes per leaf block) when its waves
+// would occupy at most BA_CASC_LAT_WAVES of the 1,024 SIMDs: there each SIMD
+// runs at most one wave and a lane's chain of Philox calls is the launch's time,
+// which the mode halves.  Above it (a whole n=16, m=5 instance: 546 waves, or
+// 1,365 in latency mode) SIMDs would take two latency-mode waves and the mode
+// loses (18.4 vs 16.5 us per instance, profiles/r04m_lat_ab.log).  BA_CASC_LAT=1/0
+// (read per call; A/B) forces it on or off where the shape has it.
+#ifndef BA_CASC_LAT_WAVES
+#define BA_CASC_LAT_WAVES 768
+#endif
+static bool use_lat(uint32_t units, uint32_t gpw_lat) {
+    const char* e = getenv("BA_CASC_LAT");
+    if (e) return e[0] != '0';
+    return (units + gpw_lat - 1) / gpw_lat <= BA_CASC_LAT_WAVES;
+}
+
 // The two-launch fan-in by k_cascade_mtop (one hand-off fewer) or k_cascade_top.
 // BA_CASC_MTOP=1/0 (read per call; A/B) forces one.
 static bool use_mtop() {
@@ -852,6 +1030,8 @@ static bool use_mtop() {
 // and that have the two-launch mode (me >= 4)
 #define BA_CASC_RANGE_SHAPES(X) X(16, 5) X(16, 4) X(9, 4) X(8, 5)
 #define BA_CASC_TWO_SHAPES(X) X(16, 5) X(16, 4) X(9, 4) X(8, 5)
+// two-launch shapes with the latency mode (odd S = n - me: leaf_half)
+#define BA_CASC_LAT_SHAPES(X) X(16, 5) X(9, 4) X(8, 5)
 // CHECK builds (tests only): depth 5 at two fan-outs, and a root-only cascade
 #define BA_CASC_CHECK_SHAPES(X) X(16, 5) X(8, 5) X(10, 3)
 
@@ -887,14 +1067,14 @@ bool cascade_range_supported(const Geometry& g, uint32_t h) {
     return shape && (h == 1 || h == 2) && h + 3 <= g.me;
 }
 
-template <int N, int ME, int DIAG = 0, bool CHECK = false>
+template <int N, int ME, int DIAG = 0, bool CHECK = false, bool LAT = false>
 static hipError_t launch_cascade_t(CascArgs& ca, hipStream_t st) {
-    using C = Casc<N, ME>;
-    constexpr uint32_t per_block = kCascWaves * C::GPW;
+    using U = CascU<N, ME, LAT>;
+    constexpr uint32_t per_block = kCascWaves * U::GPW;
     const uint32_t blocks = (ca.units + per_block - 1) / per_block;
-    const size_t lds = (size_t)(C::planes_words + kCascWaves * C::tr_words) * sizeof(uint64_t);
-    hipLaunchKernelGGL((k_cascade<N, ME, DIAG, CHECK>), dim3(blocks ? blocks : 1), dim3(64 * kCascWaves), lds,
-                       st, ca);
+    const size_t lds = (size_t)(U::planes_words + kCascWaves * U::tr_words) * sizeof(uint64_t);
+    hipLaunchKernelGGL((k_cascade<N, ME, DIAG, CHECK, LAT>), dim3(blocks ? blocks : 1), dim3(64 * kCascWaves),
+                       lds, st, ca);
     return hipGetLastError();
 }
 
@@ -942,6 +1122,7 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
     ca.cnt_off[g.me - 3] = coff;  // root counters
     ca.h = job.h;
     ca.ub = job.ub;
+    ca.ue = job.ue;
     ca.votes = job.votes;
     ca.decisions = a.decisions ? a.decisions + trial0 : nullptr;
     ca.outcome = a.outcome ? a.outcome + trial0 : nullptr;
@@ -981,21 +1162,37 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
 #undef BA_CASC_ROOT_LAUNCH
         return hipErrorInvalidValue;
     }
-    if (job.two && job.h == 0 && g.me >= 4) {
+    if (job.two && g.me >= 4 && (job.h == 0 || cascade_range_two_supported(g, job.h))) {
         // two launches: the units (k_cascade, DIAG 2: no fan-in), then the fan-in
         // from level me-3 up (k_cascade_top), one wave per level-(me-4) slot
         {
-            ProfScope ps(a.prof, "k_cascade_units", a.stream);
+            bool lat = false;
+            uint32_t gpw_lat = 0;
+#define BA_CASC_LAT_OK(nn, mm) if (g.n == nn && g.me == mm) gpw_lat = CascU<nn, mm, true>::GPW;
+            BA_CASC_LAT_SHAPES(BA_CASC_LAT_OK)
+#undef BA_CASC_LAT_OK
+            lat = gpw_lat && use_lat(ca.units, gpw_lat);
+            ProfScope ps(a.prof, lat ? "k_cascade_units_lat" : "k_cascade_units", a.stream);
             hipError_t e = hipErrorInvalidValue;
-#define BA_CASC_UNITS_LAUNCH(nn, mm) \
-    if (g.n == nn && g.me == mm) e = job.check ? launch_cascade_t<nn, mm, 2, true>(ca, a.stream) \
-                                               : launch_cascade_t<nn, mm, 2>(ca, a.stream);
-            BA_CASC_TWO_SHAPES(BA_CASC_UNITS_LAUNCH)
+#define BA_CASC_UNITS_LAUNCH(nn, mm)                                                         \
+    if (g.n == nn && g.me == mm)                                                           \
+        e = job.check ? launch_cascade_t<nn, mm, 2, true>(ca, a.stream)                    \
+                      : launch_cascade_t<nn, mm, 2>(ca, a.stream);
+#define BA_CASC_LAT_LAUNCH(nn, mm)                                                           \
+    if (g.n == nn && g.me == mm)                                                           \
+        e = job.check ? launch_cascade_t<nn, mm, 2, true, true>(ca, a.stream)              \
+                      : launch_cascade_t<nn, mm, 2, false, true>(ca, a.stream);
+            if (lat) {
+                BA_CASC_LAT_SHAPES(BA_CASC_LAT_LAUNCH)
+            } else {
+                BA_CASC_TWO_SHAPES(BA_CASC_UNITS_LAUNCH)
+            }
+#undef BA_CASC_LAT_LAUNCH
 #undef BA_CASC_UNITS_LAUNCH
             if (e != hipSuccess) return e;
         }
         CascArgs ct = ca;
-        if (use_wtop(false)) {
+        if (use_wtop(false) && job.h == 0) {
             ProfScope ps(a.prof, "k_cascade_wtop", a.stream);
 #define BA_CASC_WTOP_LAUNCH(nn, mm)                                                          \
     if (g.n == nn && g.me == mm)                                                           \
@@ -1005,12 +1202,22 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
 #undef BA_CASC_WTOP_LAUNCH
             return hipErrorInvalidValue;
         }
-        if (use_mtop()) {
+        if (use_mtop() || job.h != 0) {  // the range mode's fan-in is k_cascade_mtop's
             ProfScope ps(a.prof, "k_cascade_mtop", a.stream);
 #define BA_CASC_MTOP_LAUNCH(nn, mm)                                                                   \
     if (g.n == nn && g.me == mm) {                                                                  \
         using M = CascMtop<nn, mm>;                                                                 \
-        const dim3 grid((uint32_t)(W * M::PB)), blk(64 * M::NWV);                                    \
+        if (job.h == 0) {                       /* every level-(me-5) slot */                       \
+            ct.s0b = 0;                                                                             \
+            ct.s0n = M::PB;                                                                         \
+        } else if (job.h + 1 == (uint32_t)M::Q) { /* votes at step Q-1: s0 = the h-hop subtrees */  \
+            ct.s0b = job.ub;                                                                        \
+            ct.s0n = job.ue - job.ub;                                                               \
+        } else {                                /* h = Q: the s0 over the range's sigmas */         \
+            ct.s0b = job.ub / (uint32_t)M::NG;                                                      \
+            ct.s0n = (job.ue - 1) / (uint32_t)M::NG - ct.s0b + 1;                                   \
+        }                                                                                           \
+        const dim3 grid((uint32_t)(W * ct.s0n)), blk(64 * M::NWV);                                   \
         if (job.check)                                                                              \
             hipLaunchKernelGGL((k_cascade_mtop<nn, mm, true>), grid, blk, 0, a.stream, ct);          \
         else                                                                                        \
@@ -1058,6 +1265,16 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
     BA_CASC_SHAPES(BA_CASC_LAUNCH)
 #undef BA_CASC_LAUNCH
     return hipErrorInvalidValue;
+}
+
+// the range mode in two launches (units, then k_cascade_mtop): me >= 4 and the
+// vote level h at step me-3 or me-4
+bool cascade_range_two_supported(const Geometry& g, uint32_t h) {
+    bool shape = false;
+#define BA_CASC_OK(nn, mm) if (g.n == nn && g.me == mm) shape = true;
+    BA_CASC_TWO_SHAPES(BA_CASC_OK)
+#undef BA_CASC_OK
+    return shape && cascade_range_supported(g, h) && g.me >= 4 && h + 4 >= g.me && h + 3 <= g.me;
 }
 
 bool cascade_check_supported(const Geometry& g) {

@@ -166,6 +166,7 @@ struct CascJob {
 bool cascade_supported(const Geometry& g);
 bool cascade_check_supported(const Geometry& g);
 bool cascade_range_supported(const Geometry& g, uint32_t h);
+bool cascade_range_two_supported(const Geometry& g, uint32_t h);
 uint64_t cascade_counters_per_word(const Geometry& g);       // 128-B counters per trial word
 uint64_t cascade_scratch_words_per_word(const Geometry& g);  // R_1..R_{me-2} words per trial word (x2 with check tags)
 hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_sender,

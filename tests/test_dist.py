@@ -341,11 +341,15 @@ def test_split_votes_single_units_through_cascade(engine, monkeypatch, n, m, lev
     cascade shape with h <= m_eff - 3): ranges of ONE h-hop subtree (the fewest
     units per word, so a block's units span several words), two-subtree ranges, at
     batch 1 and 130; rows equal the oracle's, equal the multi-launch pipeline's
-    (BA_NO_CASCADE=1), and the profile shows k_cascade ran."""
+    (BA_NO_CASCADE=1), and the profile shows k_cascade ran: in one launch
+    (BA_CASC_TWO=0), and in two -- the units, then k_cascade_mtop ending at the vote
+    level -- with the units in the normal and in the latency mode (BA_CASC_LAT)."""
     from ba_amd import lib as L
     dev = torch.device("cuda", 0)
     s = torch.cuda.current_stream(dev).cuda_stream
     per = n - 1 - level
+    modes = {"one": ("0", "0", "0"), "two": ("0", "1", "0"), "two_lat": ("0", "1", "1"), "multi": ("1", "0", "0")}
+    lat_shape = (n, m) in ((16, 5), (9, 4), (8, 5))
     for B in (1, 130):
         kw = dict(seed=17 + B, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1,
                   order_mode=L.ORDER_RANDOM, first_trial=64 * 9)
@@ -355,19 +359,25 @@ def test_split_votes_single_units_through_cascade(engine, monkeypatch, n, m, lev
         for ub in units:
             for ue in (ub + 1, min(ub + 2, L.split_units(n, m, level))):
                 got = {}
-                for casc in ("1", "0"):
-                    monkeypatch.setenv("BA_NO_CASCADE", "0" if casc == "1" else "1")
+                for mode, (nocasc, two, lat) in modes.items():
+                    monkeypatch.setenv("BA_NO_CASCADE", nocasc)
+                    monkeypatch.setenv("BA_CASC_TWO", two)
+                    monkeypatch.setenv("BA_CASC_LAT", lat)
                     v = torch.zeros(((ue - ub) * per, W), dtype=torch.int64, device=dev)
                     engine.profile(True)
                     engine.split_votes_device(p, B, level, ub, ue, v.data_ptr(), stream=s)
                     torch.cuda.synchronize()
                     prof = engine.profile_read()
                     engine.profile(False)
-                    assert any("k_cascade" in k for k in prof) == (casc == "1"), prof
-                    got[casc] = v.cpu().numpy().view(np.uint64)
-                assert np.array_equal(got["1"], oracle_c.pack_votes(v_or, ub, ue)), (B, ub, ue)
-                assert np.array_equal(got["1"], got["0"])
-    monkeypatch.delenv("BA_NO_CASCADE")
+                    assert any("k_cascade" in k for k in prof) == (mode != "multi"), prof
+                    assert ("k_cascade_mtop" in prof) == mode.startswith("two"), (mode, prof)
+                    assert ("k_cascade_units_lat" in prof) == (mode == "two_lat" and lat_shape), (mode, prof)
+                    got[mode] = v.cpu().numpy().view(np.uint64)
+                assert np.array_equal(got["one"], oracle_c.pack_votes(v_or, ub, ue)), (B, ub, ue)
+                for mode in modes:
+                    assert np.array_equal(got[mode], got["one"]), (mode, B, ub, ue)
+    for k in ("BA_NO_CASCADE", "BA_CASC_TWO", "BA_CASC_LAT"):
+        monkeypatch.delenv(k)
 
 
 @pytest.mark.gpu

@@ -181,7 +181,7 @@ def test_cascade_scratch_budget_counts_counters(monkeypatch, n, m, budget_words)
         mem = eng.memory()
         assert mem["budget"] == budget
         assert 0 < mem["scratch"] + mem["counters"] <= budget, mem
-        units = [v[0] for k, v in prof.items() if k in ("k_cascade", "k_cascade_units")]
+        units = [v[0] for k, v in prof.items() if k in ("k_cascade", "k_cascade_units", "k_cascade_units_lat")]
         assert units and units[0] >= 3, prof  # chunked
         _check(res, n, m, B, **kw)
     finally:
@@ -259,6 +259,43 @@ def test_fanin_variants_agree(engine, monkeypatch, n, m, B):
         _check(out["mtop"], n, m, B, **kw)
 
 
+@pytest.mark.parametrize("n,m,B", [(16, 5, 1), (16, 5, 64), (16, 5, 130), (9, 4, 1), (9, 4, 700), (8, 5, 1),
+                                   (8, 5, 333)])
+def test_latency_mode_units_agree(engine, monkeypatch, n, m, B):
+    """The units launch in latency mode (BA_CASC_LAT=1: two lanes per leaf block,
+    the second in mirrored member labels, partial counts combined across the lane
+    pair) and in the normal mode (one lane per leaf block) give the same bits, and
+    the oracle's; the profile shows which units kernel ran."""
+    from ba_amd import lib as L
+    kw = dict(seed=0x1A7 + B, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1, order_mode=L.ORDER_RANDOM,
+              first_trial=64 * 11)
+    monkeypatch.setenv("BA_CASC_TWO", "1")
+    out = {}
+    for lat in ("1", "0"):
+        monkeypatch.setenv("BA_CASC_LAT", lat)
+        engine.profile(True)
+        out[lat] = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
+        prof = engine.profile_read()
+        engine.profile(False)
+        assert ("k_cascade_units_lat" in prof) == (lat == "1") and ("k_cascade_units" in prof) == (lat == "0"), prof
+    same(out["1"].decisions, out["0"].decisions, "decisions")
+    same(out["1"].outcome, out["0"].outcome, "outcome")
+    assert out["1"].counters == out["0"].counters
+    if B <= 130:
+        _check(out["1"], n, m, B, **kw)
+
+
+def test_latency_mode_handoff_tags(engine, monkeypatch):
+    """The latency-mode units in the check build: the fan-in reads every child with
+    this call's epoch (40 calls, batch 1 and 64)."""
+    monkeypatch.setenv("BA_CASC_TWO", "1")
+    monkeypatch.setenv("BA_CASC_LAT", "1")
+    monkeypatch.setenv("BA_CASC_CHECK", "1")
+    mism, cnt, _ = _check_calls(engine, 16, 5, (1, 64), 40, 1)
+    assert int(mism.sum()) == 0
+    assert (cnt[:, 0] > 0).all()
+
+
 def _fuzz_cases(k=24, seed=0xF022):
     rng = np.random.default_rng(seed)
     shapes = SHAPES
@@ -269,6 +306,7 @@ def _fuzz_cases(k=24, seed=0xF022):
         mode = int(rng.integers(3))  # 0 random faulty sets, 1 exact f, 2 given inputs
         two = str(rng.integers(2))
         fanin = list(FANIN)[int(rng.integers(len(FANIN)))]
+        fanin += "+lat" if rng.integers(2) else ""
         out.append((i, n, m, B, mode, two, fanin, int(rng.integers(0, 50)), int(rng.integers(1 << 30))))
     return out
 
@@ -282,8 +320,9 @@ def test_cascade_fuzz_vs_oracle(engine, monkeypatch, i, n, m, B, mode, two, fani
     oracle on decisions, outcome bytes and counters."""
     from ba_amd import lib as L
     monkeypatch.setenv("BA_CASC_TWO", two)
-    for k, v in FANIN[fanin].items():
+    for k, v in FANIN[fanin.split("+")[0]].items():
         monkeypatch.setenv(k, v)
+    monkeypatch.setenv("BA_CASC_LAT", "1" if fanin.endswith("+lat") else "0")
     if mode == 2:
         rng = np.random.default_rng(sd)
         fm = (rng.integers(0, 1 << n, B, dtype=np.uint64) & rng.integers(0, 1 << n, B, dtype=np.uint64)
