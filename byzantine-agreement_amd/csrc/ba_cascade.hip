@@ -787,11 +787,11 @@ struct CascMtop {
 };
 
 template <int N, int ME, bool CHECK = false>
-__global__ __launch_bounds__(64 * kCascWaves) void k_cascade_mtop(CascArgs a) {
+__global__ __launch_bounds__(256) void k_cascade_mtop(CascArgs a) {
     using C = Casc<N, ME>;
     using M = CascMtop<N, ME>;
     constexpr int L = M::L, Q = M::Q, K = M::K, NG = M::NG, GW = M::GW, NIN = C::NIN;
-    static_assert(Q >= 1 && M::NWV <= (int)kCascWaves, "k_cascade_mtop: me >= 4, <= 4 waves");
+    static_assert(Q >= 1 && M::NWV <= 4, "k_cascade_mtop: me >= 4, <= 4 waves");
     __shared__ __attribute__((aligned(16))) uint64_t planes[(NIN + 1) & ~1];
     __shared__ __attribute__((aligned(16))) uint64_t xch[M::NWV * GW * M::XW];
     __shared__ __attribute__((aligned(16))) uint64_t rv[NG * K];  // R_Q of s0's sigmas
