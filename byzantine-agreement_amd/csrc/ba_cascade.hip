@@ -620,7 +620,18 @@ __global__ __launch_bounds__(64 * kCascWaves, BA_CASC_MINB(N, ME, DIAG)) void k_
     const RP rp(rho, rho * (uint32_t)G);
     if (act) {
         mem = a.members[sr];
-        lie_pairs<NPD>(a.seed, ME - 1, (sr * (uint32_t)S) >> 1, gw, lw);
+        if constexpr (LAT) {  // the slot's diagonal pairs split over its two lanes, swapped by DPP
+            constexpr int NH = (NPD + 1) / 2;
+            uint64_t mine[2 * NH], other[2 * NH];
+            lie_pairs<NH>(a.seed, ME - 1, ((sr * (uint32_t)S) >> 1) + hh * (uint32_t)NH, gw, mine);
+            static_for<0, 2 * NH>([&](auto i) { other[i()] = swap_pair64(mine[i()]); });
+            static_for<0, 2 * NPD>([&](auto k) {
+                if constexpr (k() < 2 * NH) lw[k()] = hh ? other[k()] : mine[k()];
+                else lw[k()] = hh ? mine[k() - 2 * NH] : other[k() - 2 * NH];
+            });
+        } else {
+            lie_pairs<NPD>(a.seed, ME - 1, (sr * (uint32_t)S) >> 1, gw, lw);
+        }
         relay_draw<N, Q + 1, G, GL>(a, rp, xch, y, true, gw);
     }
     // 2. inputs
