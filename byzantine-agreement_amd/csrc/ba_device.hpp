@@ -49,10 +49,12 @@ __host__ __device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32
 // 2 x xor3 (tools/philox_bench: 9.5e11 calls/s on one MI355X vs 7.8e11 with
 // 2-input xors).  The key is kernel-uniform; where its round keys live is a
 // build choice of philox10_n (same results on every path):
-//   default           groups of 2-4 calls: round keys as VGPR operands (KeysV,
-//                     philox10_n_vk; a VALU op with an SGPR operand issues
-//                     slower), rounds 2-9 as one generated asm
-//                     statement (ba_philox_asm.hpp)
+//   default           groups of 2-4 calls: round keys AND the two multipliers as
+//                     VGPR operands (KeysV, philox10_n_vk; a VALU op with an SGPR
+//                     operand issues slower; VGPR multipliers:
+//                     +2.4% calls/s in tools/philox_bench, BA_PHILOX_MSGPR keeps
+//                     them in SGPRs), rounds 2-9 as one generated asm statement
+//                     (ba_philox_asm.hpp)
 //   BA_PHILOX_SKEYS   groups of 2-4 calls: round keys in SGPRs, rounds 0-1 in
 //                     C, rounds 2-9 as the asm statement
 //   G = 1 (and any    the generic round loop, keys in SGPRs, products pinned
@@ -190,6 +192,9 @@ __device__ __forceinline__ uint32_t as_vgpr(uint32_t k) {
 // asm keeps the (uniform) values in VGPRs.
 struct KeysV {
     uint32_t k0[10], k1[10];
+#ifndef BA_PHILOX_MSGPR
+    uint32_t m0, m1;  // the multipliers as VGPR operands too (BA_PHILOX_MSGPR: SGPRs, A/B)
+#endif
     __device__ __forceinline__ explicit KeysV(uint64_t seed)
         : KeysV((uint32_t)seed, (uint32_t)(seed >> 32)) {}
     // the asm is not volatile: a pure function of the seed, so the compiler can
@@ -201,6 +206,11 @@ struct KeysV {
             k1[i] = b + (uint32_t)i * 0xBB67AE85u;
             asm("" : "+v"(k0[i]), "+v"(k1[i]));
         }
+#ifndef BA_PHILOX_MSGPR
+        m0 = 0xD2511F53u;
+        m1 = 0xCD9E8D57u;
+        asm("" : "+v"(m0), "+v"(m1));
+#endif
     }
 };
 
@@ -234,7 +244,11 @@ __device__ __forceinline__ void philox10_n_vk(P4 (&c)[G], const KeysV& kv) {
             z[g] = c[g].z;
             w[g] = c[g].w;
         }
+#ifndef BA_PHILOX_MSGPR
+        philox_r29_asm_vkm<G>(x, y, z, w, rk0, rk1, kv.m0, kv.m1);
+#else
         philox_r29_asm_vk<G>(x, y, z, w, rk0, rk1);
+#endif
 #pragma unroll
         for (int g = 0; g < G; ++g) c[g] = P4{x[g], y[g], z[g], w[g]};
     } else {

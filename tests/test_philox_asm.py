@@ -100,7 +100,7 @@ def run_asm(lines, outs, ins, env):
     return out
 
 
-@pytest.mark.parametrize("name", ["philox_r29_asm", "philox_r29_asm_vk"])
+@pytest.mark.parametrize("name", ["philox_r29_asm", "philox_r29_asm_vk", "philox_r29_asm_vkm"])
 @pytest.mark.parametrize("G", [2, 3, 4])
 def test_generated_rounds_match_philox(G, name):
     lines, outs, ins = parse(G, name)
@@ -110,7 +110,7 @@ def test_generated_rounds_match_philox(G, name):
         ctrs = [[rng.getrandbits(32) for _ in range(4)] for _ in range(G)]
         r2 = [philox_rounds(c, k0, k1, 0, 2) for c in ctrs]
         want = [philox_rounds(c, k0, k1, 0, 10) for c in ctrs]
-        env = {}
+        env = {"m0": M0, "m1": M1}  # the _vkm variant's VGPR multipliers
         for g in range(G):
             env[f"x[{g}]"], env[f"yi[{g}]"], env[f"z[{g}]"], env[f"wi[{g}]"] = r2[g]
         for i in range(8):

@@ -32,7 +32,7 @@ import os
 MODE = os.environ.get("PHILOX_ASM_MODE", "rot")  # "rot": 3 pairs per call; "pairs4": 4
 
 
-def gen(G: int, kc: str = "s") -> str:
+def gen(G: int, kc: str = "s", mc: str = "s") -> str:
     # operand numbering: outputs first (x[g], z[g] in/out; w[g], y[g] fixed), then
     # inputs (y_in[g], w_in[g], keys k0[0..7], k1[0..7], M0, M1), cc last output
     ops_out, ops_in = [], []
@@ -59,8 +59,12 @@ def gen(G: int, kc: str = "s") -> str:
         ops_in.append(f'"{kc}"(k0[{i}])')
     for i in range(8):
         ops_in.append(f'"{kc}"(k1[{i}])')
-    ops_in.append('"s"(0xD2511F53u)')
-    ops_in.append('"s"(0xCD9E8D57u)')
+    if mc == "s":
+        ops_in.append('"s"(0xD2511F53u)')
+        ops_in.append('"s"(0xCD9E8D57u)')
+    else:  # the multipliers as VGPR operands too (the caller holds them in VGPRs)
+        ops_in.append('"v"(m0)')
+        ops_in.append('"v"(m1)')
     X = lambda g: g
     Z = lambda g: G + g
     CC = 4 * G
@@ -132,11 +136,12 @@ def gen(G: int, kc: str = "s") -> str:
     for g in range(G):
         ops_out = [o.replace(f"vW{g}}}", f"v{outs_w[g]}}}").replace(f"vY{g}}}", f"v{outs_y[g]}}}") for o in ops_out]
     body = "\n".join(f'        "{l}\\n\\t"' for l in lines[:-1]) + f'\n        "{lines[-1]}"'
-    fname = "philox_r29_asm" if kc == "s" else "philox_r29_asm_vk"
+    fname = "philox_r29_asm" if kc == "s" else ("philox_r29_asm_vk" if mc == "s" else "philox_r29_asm_vkm")
+    mparams = "" if mc == "s" else ",\n                                                 uint32_t m0, uint32_t m1"
     return f"""template <>
 __device__ __forceinline__ void {fname}<{G}>(uint32_t (&x)[{G}], uint32_t (&y)[{G}],
                                                  uint32_t (&z)[{G}], uint32_t (&w)[{G}],
-                                                 const uint32_t (&k0)[8], const uint32_t (&k1)[8]) {{
+                                                 const uint32_t (&k0)[8], const uint32_t (&k1)[8]{mparams}) {{
     uint32_t yi[{G}], wi[{G}];
     uint64_t cc;
     for (int g = 0; g < {G}; ++g) {{ yi[g] = y[g]; wi[g] = w[g]; }}
@@ -168,12 +173,20 @@ def main():
            '__device__ __forceinline__ void philox_r29_asm_vk(uint32_t (&x)[G], uint32_t (&y)[G],',
            '                                                  uint32_t (&z)[G], uint32_t (&w)[G],',
            '                                                  const uint32_t (&k0)[8], const uint32_t (&k1)[8]);',
+           '// the same with the multipliers as VGPR operands as well',
+           'template <int G>',
+           '__device__ __forceinline__ void philox_r29_asm_vkm(uint32_t (&x)[G], uint32_t (&y)[G],',
+           '                                                   uint32_t (&z)[G], uint32_t (&w)[G],',
+           '                                                   const uint32_t (&k0)[8], const uint32_t (&k1)[8],',
+           '                                                   uint32_t m0, uint32_t m1);',
            '']
     out.append('#ifdef __HIP_DEVICE_COMPILE__  // device code only (host passes never call it)')
     for G in (2, 3, 4):
         out.append(gen(G))
     for G in (2, 3, 4):
         out.append(gen(G, "v"))
+    for G in (2, 3, 4):
+        out.append(gen(G, "v", "v"))
     out.append('#endif')
     out.append('}  // namespace ba')
     print("\n".join(out))
