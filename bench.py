@@ -61,8 +61,9 @@ VALU_ISSUE_CYCLES = 2  # one wave64 VALU instruction per 2 cycles on a SIMD-32 (
 # Philox4x32-10 issue ceilings of one MI355X (tools/philox_bench.hip: the best
 # measured code shape per occupancy -- round 3: the kernels' grouped asm rounds
 # with the keys as VGPR operands) by resident waves per SIMD
-PHILOX_PEAK_SRC = "profiles/r03h_philox_bench.jsonl"
-PHILOX_PEAK_FALLBACK = {8: 9.69e11}
+# the code shape the kernels ship: round keys and multipliers as VGPR operands
+PHILOX_PEAK_SRC = "profiles/r04r_philox_bench_mvgpr.jsonl"
+PHILOX_PEAK_FALLBACK = {2: 9.81e11, 4: 1.048e12, 8: 1.095e12}
 PHILOX_BENCH_INSTS_PER_CALL = 40  # xor3 variant: 10 rounds x (2 v_mad_u64_u32 + 2 v_bitop3)
 # bytes one trial's own inputs and outputs occupy: faulty mask (u32) + order (u8)
 # read, decision word (u64) + outcome byte written (include/ba.h)
