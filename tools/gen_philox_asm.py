@@ -30,6 +30,8 @@ usage: python3 tools/gen_philox_asm.py > byzantine-agreement_amd/csrc/ba_philox_
 BASE = 0  # first fixed VGPR
 import os
 MODE = os.environ.get("PHILOX_ASM_MODE", "rot")  # "rot": 3 pairs per call; "pairs4": 4
+# lab: carry-out SGPR pairs the v_mad_u64_u32s rotate through (1 = one shared pair)
+NCC = int(os.environ.get("PHILOX_ASM_NCC", "1"))
 
 
 def gen(G: int, kc: str = "s", mc: str = "s") -> str:
@@ -49,7 +51,8 @@ def gen(G: int, kc: str = "s", mc: str = "s") -> str:
         ops_out.append(f'"=&{{vW{g}}}"(w[{g}])')
     for g in range(G):
         ops_out.append(f'"=&{{vY{g}}}"(y[{g}])')
-    ops_out.append('"=&s"(cc)')
+    for q in range(NCC):
+        ops_out.append(f'"=&s"(cc[{q}])' if NCC > 1 else '"=&s"(cc)')
     nout = len(ops_out)
     for g in range(G):
         ops_in.append(f'"v"(yi[{g}])')
@@ -68,7 +71,13 @@ def gen(G: int, kc: str = "s", mc: str = "s") -> str:
     X = lambda g: g
     Z = lambda g: G + g
     CC = 4 * G
-    YI = lambda g: nout + g
+    ccn = [0]
+
+    def cc():  # the next carry-out operand
+        r = CC + ccn[0] % NCC
+        ccn[0] += 1
+        return r
+    YI = lambda g: nout + g  # noqa: E731
     WI = lambda g: nout + G + g
     K0 = lambda i: nout + 2 * G + i
     K1 = lambda i: nout + 2 * G + 8 + i
@@ -88,7 +97,7 @@ def gen(G: int, kc: str = "s", mc: str = "s") -> str:
         for i in range(8):
             f = [free[g].pop(0) for g in range(G)]
             for g in range(G):   # p0 = M0 * x
-                lines.append(f"v_mad_u64_u32 v[{f[g]}:{f[g] + 1}], %{CC}, {xr[g]}, %{M0}, 0")
+                lines.append(f"v_mad_u64_u32 v[{f[g]}:{f[g] + 1}], %{cc()}, {xr[g]}, %{M0}, 0")
             for g in range(G):   # z' = hi(p0) ^ w ^ k1, into x's register
                 wprev = f"%{WI(g)}" if pw[g] is None else f"v{pw[g]}"
                 lines.append(f"v_bitop3_b32 {xr[g]}, v{f[g] + 1}, {wprev}, %{K1(i)} bitop3:0x96")
@@ -96,7 +105,7 @@ def gen(G: int, kc: str = "s", mc: str = "s") -> str:
                     free[g].append(pw[g])
             q = [free[g].pop(0) for g in range(G)]
             for g in range(G):   # p1 = M1 * z
-                lines.append(f"v_mad_u64_u32 v[{q[g]}:{q[g] + 1}], %{CC}, {zr[g]}, %{M1}, 0")
+                lines.append(f"v_mad_u64_u32 v[{q[g]}:{q[g] + 1}], %{cc()}, {zr[g]}, %{M1}, 0")
             for g in range(G):   # x' = hi(p1) ^ y ^ k0, into z's register
                 yprev = f"%{YI(g)}" if py[g] is None else f"v{py[g]}"
                 lines.append(f"v_bitop3_b32 {zr[g]}, v{q[g] + 1}, {yprev}, %{K0(i)} bitop3:0x96")
@@ -143,7 +152,7 @@ __device__ __forceinline__ void {fname}<{G}>(uint32_t (&x)[{G}], uint32_t (&y)[{
                                                  uint32_t (&z)[{G}], uint32_t (&w)[{G}],
                                                  const uint32_t (&k0)[8], const uint32_t (&k1)[8]{mparams}) {{
     uint32_t yi[{G}], wi[{G}];
-    uint64_t cc;
+    uint64_t cc{"[" + str(NCC) + "]" if NCC > 1 else ""};
     for (int g = 0; g < {G}; ++g) {{ yi[g] = y[g]; wi[g] = w[g]; }}
     asm volatile(
 {body}
