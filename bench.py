@@ -244,9 +244,9 @@ def clock_from_probes(p0, p1):
     (d s_memtime / d s_memrealtime) x 100 MHz, rows {xcc, hw, memtime, realtime}.
     s_memtime is a per-shader-engine counter, so a difference is only taken between
     rows of the SAME XCD, shader engine and CU (HW_ID bits 8-15: CU, SH, SE) in the
-    two probes; the XCD's clock is the median over those pairs.  An XCD with no CU
-    in common falls back to the median row of each probe (counters of different
-    engines: less exact).  Returns (median MHz over XCDs, {xcc: MHz})."""
+    two probes; the XCD's clock is the median over those pairs.  An XCD whose probe
+    blocks landed on no common CU is left out (a difference across engines is not a
+    clock).  Returns (median MHz over the XCDs measured, {xcc: MHz})."""
     import statistics
 
     def by_unit(rows):
@@ -255,27 +255,13 @@ def clock_from_probes(p0, p1):
             d.setdefault((int(xcc), int(hw) & 0xFF00), []).append((int(mt), int(rt)))
         return {k: sorted(v)[len(v) // 2] for k, v in d.items()}
 
-    def per_xcc(rows):
-        d = {}
-        for xcc, _, mt, rt in rows:
-            d.setdefault(int(xcc), []).append((int(mt), int(rt)))
-        return {k: sorted(v)[len(v) // 2] for k, v in d.items()}
-
     ua, ub = by_unit(p0), by_unit(p1)
     pairs = {}
     for key in set(ua) & set(ub):
         dmt, drt = ub[key][0] - ua[key][0], ub[key][1] - ua[key][1]
         if drt > 0 and dmt > 0:
             pairs.setdefault(key[0], []).append(dmt / drt * 100.0)
-    mhz = {k: round(statistics.median(v), 1) for k, v in pairs.items()}
-    a, b = per_xcc(p0), per_xcc(p1)
-    for k in sorted(set(a) & set(b)):
-        if k in mhz:
-            continue
-        dmt, drt = b[k][0] - a[k][0], b[k][1] - a[k][1]
-        if drt > 0 and dmt > 0:
-            mhz[k] = round(dmt / drt * 100.0, 1)
-    mhz = dict(sorted(mhz.items()))
+    mhz = {k: round(statistics.median(v), 1) for k, v in sorted(pairs.items())}
     return (statistics.median(mhz.values()) if mhz else None), mhz
 
 

@@ -44,7 +44,7 @@ EXPORTS = ["ba_version", "ba_device_count", "ba_ctx_create", "ba_ctx_destroy", "
            "ba_split_share", "ba_split_votes_device", "ba_root_from_split_votes_device",
            "ba_comm_allgather_split_votes_device", "ba_run_instance_split_level_multi",
            "ba_clock_probe_device", "ba_ctx_memory"]
-PROBE_BLOCKS = 64  # BA_PROBE_BLOCKS
+PROBE_BLOCKS = 2048  # BA_PROBE_BLOCKS
 
 
 class BAError(RuntimeError):

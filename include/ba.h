@@ -345,10 +345,12 @@ int ba_profile_read(struct ba_ctx* ctx, int index, char* name, int name_len,
 /* Engine-clock probe (measurement aux; no ba.py analogue).  Enqueues on `stream`
  * one tiny launch of BA_PROBE_BLOCKS one-wave blocks; block b writes
  * d_out[4b .. 4b+3] = {XCC id, HW id, s_memtime, s_memrealtime}.  s_memtime
- * counts shader-clock cycles, s_memrealtime a constant 100 MHz clock, so two
- * probes bracketing a stretch of work give that stretch's average engine clock
- * per XCD: (dmemtime / drealtime) x 100 MHz (MI355X_MICROARCH.md).  bench.py
- * brackets a replica of its timed region with two probes. */
+ * counts shader-clock cycles on a PER-CU counter (counters of different CUs are
+ * not aligned), s_memrealtime a constant 100 MHz clock, so two probes bracketing
+ * a stretch of work give that stretch's average engine clock per XCD from rows
+ * of the SAME CU (HW id bits 8-15): (dmemtime / drealtime) x 100 MHz
+ * (MI355X_MICROARCH.md).  BA_PROBE_BLOCKS = 2048 one-wave blocks reach every CU
+ * in each probe.  bench.py brackets a replica of its timed region with two. */
 /* Device memory a ctx holds for the engines: the LEVELS scratch and the
  * cascade's fan-in counters, and the budget both are chunked to (environment
  * BA_SCRATCH_BYTES at ba_ctx_create, 8 GiB by default): scratch + counters <=
@@ -356,7 +358,7 @@ int ba_profile_read(struct ba_ctx* ctx, int index, char* name, int name_len,
 int ba_ctx_memory(struct ba_ctx* ctx, uint64_t* scratch_bytes, uint64_t* counter_bytes,
                   uint64_t* budget_bytes);
 
-#define BA_PROBE_BLOCKS 64
+#define BA_PROBE_BLOCKS 2048
 int ba_clock_probe_device(struct ba_ctx* ctx, uint64_t* d_out, void* stream);
 
 /* ---- ba.py's coin source (host only, no device needed) --------------------

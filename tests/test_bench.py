@@ -181,11 +181,11 @@ def test_cpu_baseline_world2_gloo():
 def test_clock_from_probes_pairs_rows_by_cu():
     """The engine clock per XCD comes from rows of the same XCD, shader engine and CU
     (HW_ID bits 8-15) in the two probes; an unrelated CU's counter (another engine's
-    s_memtime) never enters a difference; an XCD with no common CU falls back to the
-    median rows."""
+    s_memtime) never enters a difference, and an XCD with no CU in both probes is
+    left out."""
     p0 = [(0, 0x0100, 1000, 10), (0, 0x0200, 900000, 10), (1, 0x0100, 5000, 10), (2, 0x0100, 7, 10)]
     p1 = [(0, 0x0100, 1000 + 2400, 110), (0, 0x0300, 10, 110), (1, 0x0100, 5000 + 2300, 110),
           (2, 0x0200, 7 + 2200, 110)]
     med, per = bench.clock_from_probes(p0, p1)
-    assert per == {0: 2400.0, 1: 2300.0, 2: 2200.0}
-    assert med == 2300.0
+    assert per == {0: 2400.0, 1: 2300.0}
+    assert med == 2350.0

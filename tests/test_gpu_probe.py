@@ -33,4 +33,4 @@ def test_clock_probe_rows_and_clock(engine):
     assert min(r[3] for r in rows[1]) > max(r[3] for r in rows[0])  # s_memrealtime: one clock
     med, per = bench.clock_from_probes(rows[0], rows[1])
     assert med is not None and 300 <= med <= 3000, (med, per)
-    assert all(100 <= v <= 3500 for v in per.values()), per
+    assert per and all(100 <= v <= 3500 for v in per.values()), (per, rows)
