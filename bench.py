@@ -379,6 +379,9 @@ def main():
         try:
             comm = D.init_comm(eng)
             collective = "rccl (libba_hip ba_comm_allreduce_device)"
+            if os.environ.get("BA_RCCL_LIB"):  # test-only replacement (tests/native/fake_rccl.c)
+                collective = ("rccl API of BA_RCCL_LIB=" + os.path.basename(os.environ["BA_RCCL_LIB"]) +
+                              " (libba_hip ba_comm_allreduce_device; a test stand-in, not RCCL)")
         except L.BAError as e:  # reported in the JSON line, never silent
             print(f"bench: RCCL communicator failed ({e}); counters all-reduced over gloo",
                   file=sys.stderr, flush=True)

@@ -21,7 +21,7 @@ ABI_VERSION = 1
 MAX_GENERALS = 32
 MAX_DEPTH = 8
 NCOUNTERS = 16
-OK, EINVAL, ENOMEM, EDEVICE, ENOTSUP, ETOOBIG = 0, -1, -2, -3, -4, -5
+OK, EINVAL, ENOMEM, EDEVICE, ENOTSUP, ETOOBIG, EABORTED = 0, -1, -2, -3, -4, -5, -6
 LIE_PHILOX, LIE_TABLE = 0, 1
 FAULTY_GIVEN, FAULTY_RANDOM, FAULTY_EXACT = 0, 1, 2
 ORDER_GIVEN, ORDER_RANDOM, ORDER_CONST = 0, 1, 2
@@ -43,7 +43,7 @@ EXPORTS = ["ba_version", "ba_device_count", "ba_ctx_create", "ba_ctx_destroy", "
            "ba_run_instance_split_multi", "ba_split_units", "ba_split_vote_slots",
            "ba_split_share", "ba_split_votes_device", "ba_root_from_split_votes_device",
            "ba_comm_allgather_split_votes_device", "ba_run_instance_split_level_multi",
-           "ba_clock_probe_device", "ba_ctx_memory"]
+           "ba_clock_probe_device", "ba_ctx_memory", "ba_comm_set_timeout", "ba_comm_abort"]
 PROBE_BLOCKS = 2048  # BA_PROBE_BLOCKS
 
 
@@ -140,6 +140,8 @@ def load(path: str | None = None):
                                         ctypes.POINTER(Counters), ctypes.POINTER(u64),
                                         ctypes.POINTER(u64)]
     lib.ba_comm_rank.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
+    lib.ba_comm_set_timeout.argtypes = [vp, u64]
+    lib.ba_comm_abort.argtypes = [vp]
     lib.ba_subtree_share.argtypes = [u32, i32, i32, ctypes.POINTER(u32), ctypes.POINTER(u32)]
     lib.ba_comm_allreduce_device.argtypes = [vp, vp, vp]
     lib.ba_comm_allgather_votes_device.argtypes = [vp, u32, u32, u64, vp, vp]
@@ -432,6 +434,16 @@ class Comm:
         """Every rank's subtree-vote rows to every rank, in place (async on stream)."""
         _check(self.lib, self.lib.ba_comm_allgather_votes_device(self.handle, n, m, batch,
                                                                  d_votes, stream or None))
+
+    def set_timeout(self, timeout_ms: int):
+        """Watchdog of the blocking jobs (ba_comm_set_timeout): past it a job aborts
+        the communicator and raises BAError(EABORTED)."""
+        _check(self.lib, self.lib.ba_comm_set_timeout(self.handle, timeout_ms))
+
+    def abort(self):
+        """ncclCommAbort on this rank (ba_comm_abort); every further call raises
+        BAError(EABORTED); close() still frees the comm."""
+        _check(self.lib, self.lib.ba_comm_abort(self.handle))
 
     def close(self):
         if self.handle:

@@ -616,6 +616,11 @@ static uint32_t cascade_check_mode(const Geometry& g) {
     return (v == 1 || v == 2) && cascade_check_supported(g) ? (uint32_t)v : 0u;
 }
 
+// run_cascade's answer when the split's one-chunk cascade does not fit the
+// scratch budget: the caller runs the per-range LEVELS kernels instead, whose
+// scratch shrinks with the rank's unit range (internal, never returned)
+constexpr int kCascadeNoFit = 1;
+
 // job.h != 0 (the subtree split): one chunk (`whole`), no counters.
 static int run_cascade(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge, CascJob job = CascJob{}) {
     const Geometry& g = ge->g;
@@ -633,19 +638,25 @@ static int run_cascade(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge, CascJob job 
     }
     // per trial word: R_1 .. R_{me-2} (twice with check tags) and the fan-in
     // counters, one 128-B line each -- both count against the scratch budget
-    const uint64_t r_bytes = cascade_scratch_words_per_word(g) * sizeof(uint64_t) * (job.check ? 2 : 1);
-    const uint64_t c_bytes = cascade_counters_per_word(g) * 128;
+    // The split's root pass as k_cascade_wtop uses neither (the default)
+    const bool uses = !job.vin || cascade_root_pass_uses_scratch();
+    const uint64_t r_bytes = uses ? cascade_scratch_words_per_word(g) * sizeof(uint64_t) *
+                                        (job.check ? 2 : 1) : 0;
+    const uint64_t c_bytes = uses ? cascade_counters_per_word(g) * 128 : 0;
     const uint64_t words = (a.batch + 63) / 64;
     uint64_t max_level = 0;
     for (uint32_t k = 0; k + 2 <= g.me; ++k) max_level = g.S[k] > max_level ? g.S[k] : max_level;
-    uint64_t chunk = ctx->scratch_budget / (r_bytes + c_bytes);
+    uint64_t chunk = uses ? ctx->scratch_budget / (r_bytes + c_bytes) : words;
     const uint64_t idx_cap = (1ull << 31) / (max_level + 1);  // 32-bit slot indices in the kernel
     if (chunk > idx_cap) chunk = idx_cap;
+    // the counter sink: one unit per word, < 2^16 units per replica (ba_device.hpp)
+    const uint64_t sink_cap = (uint64_t)kSinkReplicas * kSinkMaxUnitsPerReplica;
+    if (chunk > sink_cap) chunk = sink_cap;
     if (chunk > words) chunk = words;
-    if (chunk == 0 || (whole && chunk < words))
-        return fail(BA_ETOOBIG, "%llu 64-trial words need %llu bytes of scratch and counters each "
-                    "(budget %zu%s)", (unsigned long long)words, (unsigned long long)(r_bytes + c_bytes),
-                    ctx->scratch_budget, whole ? ", one chunk required: split the batch" : "");
+    if (whole && chunk < words) return kCascadeNoFit;
+    if (chunk == 0)
+        return fail(BA_ETOOBIG, "a 64-trial word needs %llu bytes of scratch and counters (budget "
+                    "%zu)", (unsigned long long)(r_bytes + c_bytes), ctx->scratch_budget);
     int rc;
     if ((rc = ctx->scratch.grow(chunk * r_bytes)) != BA_OK) return rc;
     const size_t cbytes = chunk * c_bytes;
@@ -786,7 +797,7 @@ static int subtree_votes_impl(ba_ctx* ctx, const ba_params* p, uint64_t batch, u
         cj.ub = j_begin;
         cj.ue = j_end;
         cj.votes = d_votes;
-        return run_cascade(ctx, a, ge, cj);
+        if ((rc = run_cascade(ctx, a, ge, cj)) != kCascadeNoFit) return rc;
     }
     LevelsJob job;
     job.root = false;
@@ -814,7 +825,7 @@ static int root_from_votes_impl(ba_ctx* ctx, const ba_params* p, uint64_t batch,
         CascJob cj;  // one launch: step level-1 from the votes, roots, quorum
         cj.vin = d_votes;
         cj.root_h = level;
-        return run_cascade(ctx, a, ge, cj);
+        if ((rc = run_cascade(ctx, a, ge, cj)) != kCascadeNoFit) return rc;
     }
     LevelsJob job;
     job.tree = false;

@@ -1009,6 +1009,9 @@ static bool use_wtop(bool root_pass) {
     if (e) return e[0] != '0';
     return root_pass;
 }
+// the split's root pass touches neither the scratch nor the fan-in counters
+// when it runs as k_cascade_wtop (one block per word, LDS only)
+bool cascade_root_pass_uses_scratch() { return !use_wtop(true); }
 // The units launch in latency mode (two lanes per leaf block) when its waves
 // would occupy at most BA_CASC_LAT_WAVES of the 1,024 SIMDs: there each SIMD
 // runs at most one wave and a lane's chain of Philox calls is the launch's time,

@@ -690,6 +690,7 @@ constexpr uint32_t kSinkReplicas = 64;
 constexpr uint32_t kSinkRepStride = 16;  // uint64 per replica (128 B)
 constexpr size_t kSinkBytes = kSinkReplicas * kSinkRepStride * 8;
 constexpr uint32_t kSinkArrivalShift = 48;
+constexpr uint32_t kSinkMaxUnitsPerReplica = (1u << (64 - kSinkArrivalShift)) - 1;  // 65535
 constexpr unsigned long long kSinkValueMask = (1ull << kSinkArrivalShift) - 1;
 
 struct Sink {

@@ -169,6 +169,7 @@ bool cascade_range_supported(const Geometry& g, uint32_t h);
 bool cascade_range_two_supported(const Geometry& g, uint32_t h);
 uint64_t cascade_counters_per_word(const Geometry& g);       // 128-B counters per trial word
 uint64_t cascade_scratch_words_per_word(const Geometry& g);  // R_1..R_{me-2} words per trial word (x2 with check tags)
+bool cascade_root_pass_uses_scratch();                       // false: k_cascade_wtop (the default)
 hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_sender,
                           uint64_t* scratch, uint32_t* d_cnt, uint64_t trial0, uint64_t ntrials,
                           const CascJob& job);

@@ -23,10 +23,22 @@
 // the counters, so no rank blocks in a collective another rank skipped and
 // every rank returns the error.
 //
+// Watchdog: a blocking whole job waits for its collectives by polling the
+// comm's stream, and past the comm's timeout aborts the communicator
+// (ncclCommAbort makes this rank's RCCL kernels return) and fails with
+// BA_EABORTED.  A rank whose own transport fails (it cannot learn the agreed
+// error flag, or cannot raise it) aborts itself at once: RCCL has no way to
+// tell the peers, so they leave through their own watchdog.  Every rank's wait
+// is bounded either way.
+//
 // RCCL is opened with dlopen on first use: torch's wheel bundles its own
 // librccl.so, and a process that imports torch keeps that copy (RTLD_NOLOAD
-// finds it) instead of loading a second RCCL beside it.
+// finds it) instead of loading a second RCCL beside it.  BA_RCCL_LIB names a
+// replacement with the same entry points (test-only: tests/native/fake_rccl.c,
+// a shared-memory stand-in that lets N processes share one GPU, which RCCL
+// refuses, so these N>1 paths run on a one-GPU box).
 #include <dlfcn.h>
+#include <time.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -53,17 +65,23 @@ struct Rccl {
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
+    decltype(&ncclCommAbort) comm_abort = nullptr;
 };
 
 Rccl& rccl() {
     static Rccl r;
     if (r.tried) return r;
     r.tried = true;
-    for (const char* name : {"librccl.so", "librccl.so.1"}) {  // already loaded (torch's) first
-        if ((r.h = dlopen(name, RTLD_NOW | RTLD_NOLOAD))) break;
+    const char* over = getenv("BA_RCCL_LIB");  // test-only replacement (see the top)
+    if (over && over[0]) {
+        r.h = dlopen(over, RTLD_NOW | RTLD_LOCAL);
+    } else {
+        for (const char* name : {"librccl.so", "librccl.so.1"}) {  // already loaded (torch's) first
+            if ((r.h = dlopen(name, RTLD_NOW | RTLD_NOLOAD))) break;
+        }
+        if (!r.h) r.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!r.h) r.h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
     }
-    if (!r.h) r.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-    if (!r.h) r.h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
     if (!r.h) return r;
     r.get_unique_id = (decltype(r.get_unique_id))dlsym(r.h, "ncclGetUniqueId");
     r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(r.h, "ncclCommInitRank");
@@ -73,8 +91,9 @@ Rccl& rccl() {
     r.group_start = (decltype(r.group_start))dlsym(r.h, "ncclGroupStart");
     r.group_end = (decltype(r.group_end))dlsym(r.h, "ncclGroupEnd");
     r.error_string = (decltype(r.error_string))dlsym(r.h, "ncclGetErrorString");
+    r.comm_abort = (decltype(r.comm_abort))dlsym(r.h, "ncclCommAbort");
     if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.all_reduce || !r.broadcast ||
-        !r.group_start || !r.group_end || !r.error_string)
+        !r.group_start || !r.group_end || !r.error_string || !r.comm_abort)
         r.h = nullptr;
     return r;
 }
@@ -89,6 +108,22 @@ int failf(int code, const char* fmt, ...) {
 }
 
 constexpr int kErrSlot = BA_NCOUNTERS - 1;  // error flag, all-reduced with the counters
+constexpr uint64_t kDefaultTimeoutMs = 300000;
+
+uint64_t now_ns() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+
+// BA_TEST_PREAGREE_FAIL (test-only, read per call): make this rank's
+// pre-exchange agreement transport fail -- "upload" (the flag upload; the
+// device memset that replaces it works), "upload_memset" (both), "readback"
+// (the agreed sum cannot be read back).
+bool test_fail(const char* what) {
+    const char* e = getenv("BA_TEST_PREAGREE_FAIL");
+    return e && strcmp(e, what) == 0;
+}
 
 }  // namespace
 
@@ -99,7 +134,50 @@ struct ba_comm {
     uint64_t* d_votes = nullptr;  // full vote array of the split (grown on demand)
     size_t votes_bytes = 0;
     hipStream_t stream = nullptr;  // the ctx's own stream (not owned: the ctx outlives the comm)
+    uint64_t* h_pin = nullptr;  // pinned host words: counter read-back, flag upload / read-back
+    uint64_t timeout_ms = kDefaultTimeoutMs;  // watchdog of the blocking jobs
+    bool aborted = false;  // ncclCommAbort ran: the RCCL communicator is gone
 };
+
+// Abort the RCCL communicator: this rank's pending collectives return (RCCL
+// kernels poll the abort flag), the communicator is freed, and every further
+// call on the comm fails with BA_EABORTED.
+static void abort_comm(ba_comm* c) {
+    if (c->aborted) return;
+    c->aborted = true;
+    if (c->comm && rccl().h) (void)rccl().comm_abort(c->comm);
+    c->comm = nullptr;
+}
+
+static int fail_aborted(const ba_comm* c) {
+    return failf(BA_EABORTED, "communicator of rank %d (of %d) was aborted; destroy it and create "
+                 "a new one", c->rank, c->nranks);
+}
+
+// Wait for the comm's stream (the blocking jobs' collectives): poll it, and
+// past the timeout abort the communicator so the stream drains, and fail.
+static int comm_wait(ba_comm* c, const char* what) {
+    const uint64_t t0 = now_ns(), lim = c->timeout_ms * 1000000ull;
+    for (uint32_t k = 0;; ++k) {
+        const hipError_t e = hipStreamQuery(c->stream);
+        if (e == hipSuccess) return BA_OK;
+        if (e != hipErrorNotReady) {
+            abort_comm(c);
+            return failf(BA_EDEVICE, "%s: %s (communicator aborted)", what, hipGetErrorString(e));
+        }
+        if (now_ns() - t0 > lim) {
+            abort_comm(c);
+            (void)hipStreamSynchronize(c->stream);  // the aborted collectives return
+            return failf(BA_EABORTED, "%s: no completion within %llu ms (a peer left the "
+                         "exchange); communicator of rank %d aborted", what,
+                         (unsigned long long)c->timeout_ms, c->rank);
+        }
+        if (k > 2000) {  // a short spin first: most jobs complete within it
+            timespec ts = {0, 50000};
+            nanosleep(&ts, nullptr);
+        }
+    }
+}
 
 // ba_api.cpp, library-internal
 extern "C" hipStream_t ba_ctx_stream_internal(struct ba_ctx* ctx);
@@ -135,7 +213,13 @@ extern "C" int ba_comm_create(struct ba_ctx* ctx, int nranks, int rank,
     // afterwards orders itself after it by an event recorded on that stream
     // (ba_api.cpp ctx_order), so the stream must live as long as the ctx
     c->stream = ba_ctx_stream_internal(ctx);
-    if (hipMalloc(&c->d_cnt, BA_NCOUNTERS * sizeof(uint64_t)) != hipSuccess) {
+    if (const char* t = getenv("BA_COMM_TIMEOUT_MS")) {
+        const uint64_t v = strtoull(t, nullptr, 0);
+        if (v > 0) c->timeout_ms = v;
+    }
+    if (hipMalloc(&c->d_cnt, BA_NCOUNTERS * sizeof(uint64_t)) != hipSuccess ||
+        hipHostMalloc(&c->h_pin, (BA_NCOUNTERS + 2) * sizeof(uint64_t), 0) != hipSuccess) {
+        if (c->d_cnt) (void)hipFree(c->d_cnt);
         delete c;
         return failf(BA_ENOMEM, "communicator buffers");
     }
@@ -144,6 +228,7 @@ extern "C" int ba_comm_create(struct ba_ctx* ctx, int nranks, int rank,
     const ncclResult_t e = r.comm_init_rank(&c->comm, nranks, u, rank);
     if (e != ncclSuccess) {
         (void)hipFree(c->d_cnt);
+        (void)hipHostFree(c->h_pin);
         delete c;
         return failf(BA_EDEVICE, "ncclCommInitRank(%d ranks, rank %d): %s", nranks, rank,
                      r.error_string(e));
@@ -156,9 +241,10 @@ extern "C" void ba_comm_destroy(struct ba_comm* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->comm && rccl().h) (void)rccl().comm_destroy(c->comm);
+    if (c->comm && !c->aborted && rccl().h) (void)rccl().comm_destroy(c->comm);
     if (c->d_cnt) (void)hipFree(c->d_cnt);
     if (c->d_votes) (void)hipFree(c->d_votes);
+    if (c->h_pin) (void)hipHostFree(c->h_pin);
     delete c;
 }
 
@@ -166,6 +252,18 @@ extern "C" int ba_comm_rank(struct ba_comm* comm, int* nranks, int* rank) {
     if (!comm) return failf(BA_EINVAL, "comm is NULL");
     if (nranks) *nranks = comm->nranks;
     if (rank) *rank = comm->rank;
+    return BA_OK;
+}
+
+extern "C" int ba_comm_set_timeout(struct ba_comm* comm, uint64_t timeout_ms) {
+    if (!comm || timeout_ms == 0) return failf(BA_EINVAL, "comm is NULL or timeout is 0");
+    comm->timeout_ms = timeout_ms;
+    return BA_OK;
+}
+
+extern "C" int ba_comm_abort(struct ba_comm* comm) {
+    if (!comm) return failf(BA_EINVAL, "comm is NULL");
+    abort_comm(comm);
     return BA_OK;
 }
 
@@ -212,6 +310,7 @@ extern "C" int ba_split_share(uint32_t n, uint32_t m, uint32_t level, int nranks
 // ---------------------------------------------------------------------------
 extern "C" int ba_comm_allreduce_device(struct ba_comm* comm, uint64_t* d_counters, void* stream) {
     if (!comm || !d_counters) return failf(BA_EINVAL, "comm and d_counters are required");
+    if (comm->aborted) return fail_aborted(comm);
     if (hipSetDevice(comm->device) != hipSuccess) return failf(BA_EDEVICE, "hipSetDevice");
     Rccl& r = rccl();
     const ncclResult_t e = r.all_reduce(d_counters, d_counters, BA_NCOUNTERS, ncclUint64, ncclSum,
@@ -226,6 +325,7 @@ extern "C" int ba_comm_allgather_split_votes_device(struct ba_comm* comm, uint32
     if (!comm || !d_votes) return failf(BA_EINVAL, "comm and d_votes are required");
     const uint64_t units = ba_split_units(n, m, level);
     if (units == 0) return failf(BA_EINVAL, "no level-%u split votes for n=%u, m=%u", level, n, m);
+    if (comm->aborted) return fail_aborted(comm);
     if (hipSetDevice(comm->device) != hipSuccess) return failf(BA_EDEVICE, "hipSetDevice");
     const uint64_t W = (batch + 63) / 64, row = (uint64_t)(n - 1 - level) * W;  // words per unit
     Rccl& r = rccl();
@@ -257,29 +357,42 @@ extern "C" int ba_comm_allgather_votes_device(struct ba_comm* comm, uint32_t n, 
 // Sum every rank's error flag -- and, for trial-DP, the counters (a split
 // computes the same whole-job counters on every rank) -- over the ranks, copy
 // them to the host and report: the local error, else "another rank failed",
-// else OK.
+// else OK.  A rank that cannot raise its flag, or whose collective cannot be
+// enqueued, aborts itself (its peers then leave through their watchdog): it
+// never returns as if nothing failed while its peers wait for it.
 static int finish_job(ba_comm* comm, int local_rc, ba_counters* counters_out, bool sum_counters) {
+    if (comm->aborted) return local_rc != BA_OK ? local_rc : fail_aborted(comm);
+    uint64_t* h = comm->h_pin;  // pinned: the copies below never block the host
     if (local_rc != BA_OK) {
-        static const uint64_t one = 1;
-        (void)hipMemcpyAsync(comm->d_cnt + kErrSlot, &one, sizeof one, hipMemcpyHostToDevice,
-                             comm->stream);
+        h[BA_NCOUNTERS] = 1;
+        if (hipMemcpyAsync(comm->d_cnt + kErrSlot, h + BA_NCOUNTERS, sizeof(uint64_t),
+                           hipMemcpyHostToDevice, comm->stream) != hipSuccess) {
+            abort_comm(comm);
+            return local_rc;
+        }
     }
-    ba_counters tmp;
+    Rccl& r = rccl();
+    const ncclResult_t e = sum_counters
+        ? r.all_reduce(comm->d_cnt, comm->d_cnt, BA_NCOUNTERS, ncclUint64, ncclSum, comm->comm,
+                       comm->stream)
+        : r.all_reduce(comm->d_cnt + kErrSlot, comm->d_cnt + kErrSlot, 1, ncclUint64, ncclSum,
+                       comm->comm, comm->stream);
+    if (e != ncclSuccess) {
+        abort_comm(comm);
+        return local_rc != BA_OK ? local_rc
+                                 : failf(BA_EDEVICE, "ncclAllReduce: %s (communicator aborted)",
+                                         r.error_string(e));
+    }
     int rc = BA_OK;
-    if (sum_counters) {
-        rc = ba_comm_allreduce_device(comm, comm->d_cnt, comm->stream);
-    } else {
-        Rccl& r = rccl();
-        const ncclResult_t e = r.all_reduce(comm->d_cnt + kErrSlot, comm->d_cnt + kErrSlot, 1,
-                                            ncclUint64, ncclSum, comm->comm, comm->stream);
-        if (e != ncclSuccess) rc = failf(BA_EDEVICE, "ncclAllReduce: %s", r.error_string(e));
-    }
-    if (hipMemcpyAsync(tmp.v, comm->d_cnt, sizeof tmp.v, hipMemcpyDeviceToHost, comm->stream) !=
-            hipSuccess ||
-        hipStreamSynchronize(comm->stream) != hipSuccess)
+    if (hipMemcpyAsync(h, comm->d_cnt, BA_NCOUNTERS * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                       comm->stream) != hipSuccess)
         rc = failf(BA_EDEVICE, "counter read-back");
+    const int rw = comm_wait(comm, "counter all-reduce");
     if (local_rc != BA_OK) return local_rc;
+    if (rw != BA_OK) return rw;
     if (rc != BA_OK) return rc;
+    ba_counters tmp;
+    memcpy(tmp.v, h, sizeof tmp.v);
     if (tmp.v[kErrSlot] != 0)
         return failf(BA_EDEVICE, "%llu other rank(s) failed this call",
                      (unsigned long long)tmp.v[kErrSlot]);
@@ -295,53 +408,75 @@ static bool force_split() {
     return e && e[0] == '1';
 }
 
-// Sum every rank's error flag now, synchronously, before a collective that a
-// failed rank could not join.  Returns BA_OK when this rank is to join the
-// exchange; otherwise this rank's own error, or "another rank failed" -- the
-// same answer on every rank, so all of them leave the call together.  The
-// error slot is left at 0 for finish_job when no rank failed.
+// Sum every rank's error flag now, before a collective that a failed rank
+// could not join.  Returns BA_OK when this rank is to join the exchange;
+// otherwise this rank's own error, or "another rank failed" -- the same answer
+// on every rank, so all of them leave the call together and the comm stays
+// usable.  The error slot is left at 0 for finish_job when no rank failed.
 // This rank's own agreement transport can fail while its local work is valid:
 //  - flag upload: the flag is raised with a device memset instead (a failed
 //    upload counts as a failure every rank sees), so all ranks leave together;
-//  - read-back: its peers read the sum and, if no rank failed, enter the
-//    exchange, so this rank joins them too and reports the error after the
-//    exchange (*late) instead of leaving them waiting in the broadcasts.
-static int preagree(ba_comm* comm, int local_rc, int* late) {
-    uint64_t flag = local_rc != BA_OK ? 1 : 0;
-    uint64_t got = 0;
+//    if the memset fails too, the flag cannot be raised at all;
+//  - the all-reduce cannot be enqueued, or the agreed sum cannot be read back:
+//    this rank cannot know whether its peers enter the exchange.
+// In those last cases the rank aborts its communicator and fails: peers that
+// wait for it in the all-reduce or the exchange leave through their watchdog
+// (comm_wait), so no rank waits forever, and none trusts a half-done exchange.
+static int preagree(ba_comm* comm, int local_rc) {
+    uint64_t* up = comm->h_pin + BA_NCOUNTERS;      // pinned flag upload
+    uint64_t* got = comm->h_pin + BA_NCOUNTERS + 1;  // pinned read-back
+    *up = local_rc != BA_OK ? 1 : 0;
+    *got = 0;
     Rccl& r = rccl();
-    int up = BA_OK;
-    if (hipMemcpyAsync(comm->d_cnt + kErrSlot, &flag, sizeof flag, hipMemcpyHostToDevice,
+    int up_rc = BA_OK;
+    if (test_fail("upload") || test_fail("upload_memset") ||
+        hipMemcpyAsync(comm->d_cnt + kErrSlot, up, sizeof *up, hipMemcpyHostToDevice,
                        comm->stream) != hipSuccess) {
-        up = failf(BA_EDEVICE, "error-flag upload");
-        flag = 1;  // raise it on the device: lowest byte 1 = a flag of 1
-        (void)hipMemsetAsync(comm->d_cnt + kErrSlot, 0, sizeof flag, comm->stream);
-        (void)hipMemsetAsync(comm->d_cnt + kErrSlot, 1, 1, comm->stream);
+        up_rc = failf(BA_EDEVICE, "error-flag upload");
+        // raise it on the device: lowest byte 1 = a flag of 1
+        if (test_fail("upload_memset") ||
+            hipMemsetAsync(comm->d_cnt + kErrSlot, 0, sizeof(uint64_t), comm->stream) != hipSuccess ||
+            hipMemsetAsync(comm->d_cnt + kErrSlot, 1, 1, comm->stream) != hipSuccess) {
+            abort_comm(comm);
+            return local_rc != BA_OK ? local_rc
+                                     : failf(BA_EABORTED, "error flag could neither be uploaded "
+                                             "nor set on the device; communicator aborted");
+        }
     }
     const ncclResult_t e = r.all_reduce(comm->d_cnt + kErrSlot, comm->d_cnt + kErrSlot, 1, ncclUint64,
                                         ncclSum, comm->comm, comm->stream);
-    if (e != ncclSuccess)  // the communicator itself failed: no exchange can follow
-        return local_rc != BA_OK ? local_rc : failf(BA_EDEVICE, "ncclAllReduce: %s", r.error_string(e));
-    if (hipMemcpyAsync(&got, comm->d_cnt + kErrSlot, sizeof got, hipMemcpyDeviceToHost,
-                       comm->stream) != hipSuccess ||
-        hipStreamSynchronize(comm->stream) != hipSuccess) {
-        if (local_rc != BA_OK || up != BA_OK) return local_rc != BA_OK ? local_rc : up;
-        *late = failf(BA_EDEVICE, "error-flag read-back");
-        (void)hipMemsetAsync(comm->d_cnt + kErrSlot, 0, sizeof got, comm->stream);
-        return BA_OK;
+    if (e != ncclSuccess) {
+        abort_comm(comm);
+        return local_rc != BA_OK ? local_rc
+                                 : failf(BA_EABORTED, "ncclAllReduce: %s (communicator aborted)",
+                                         r.error_string(e));
     }
+    if (test_fail("readback") ||
+        hipMemcpyAsync(got, comm->d_cnt + kErrSlot, sizeof *got, hipMemcpyDeviceToHost,
+                       comm->stream) != hipSuccess) {
+        abort_comm(comm);
+        return local_rc != BA_OK ? local_rc
+               : up_rc != BA_OK  ? up_rc
+                                 : failf(BA_EABORTED, "error-flag read-back; communicator aborted");
+    }
+    const int rw = comm_wait(comm, "pre-exchange error agreement");
     if (local_rc != BA_OK) return local_rc;
-    if (up != BA_OK) return up;
-    if (got != 0)
+    if (up_rc != BA_OK) return up_rc;
+    if (rw != BA_OK) return rw;
+    if (*got != 0)
         return failf(BA_EDEVICE, "%llu other rank(s) failed this call before the vote exchange",
-                     (unsigned long long)got);
+                     (unsigned long long)*got);
     return BA_OK;
 }
 
 static int begin_job(ba_comm* comm) {
-    if (hipSetDevice(comm->device) != hipSuccess) return failf(BA_EDEVICE, "hipSetDevice");
-    if (hipMemsetAsync(comm->d_cnt, 0, BA_NCOUNTERS * sizeof(uint64_t), comm->stream) != hipSuccess)
-        return failf(BA_EDEVICE, "hipMemsetAsync");
+    if (comm->aborted) return fail_aborted(comm);
+    if (hipSetDevice(comm->device) != hipSuccess || hipMemsetAsync(comm->d_cnt, 0,
+            BA_NCOUNTERS * sizeof(uint64_t), comm->stream) != hipSuccess) {
+        abort_comm(comm);  // this rank cannot take part: its peers leave through their watchdog
+        return failf(BA_EDEVICE, "rank %d cannot reach its device (communicator aborted)",
+                     comm->rank);
+    }
     return BA_OK;
 }
 
@@ -400,13 +535,15 @@ extern "C" int ba_run_instance_split_level_multi(struct ba_ctx* ctx, struct ba_c
     }
     const uint64_t W = (batch + 63) / 64;
     const size_t need = (size_t)(slots * W * sizeof(uint64_t));
-    if (local == BA_OK && need > comm->votes_bytes) {
+    const char* inj = getenv("BA_TEST_VOTE_ENOMEM");  // test-only: this call's allocation fails
+    if (local == BA_OK && inj && inj[0] == '1') {
+        local = failf(BA_ENOMEM, "vote buffer (%zu B; injected by BA_TEST_VOTE_ENOMEM)", need);
+    } else if (local == BA_OK && need > comm->votes_bytes) {
         (void)hipStreamSynchronize(comm->stream);
         if (comm->d_votes) (void)hipFree(comm->d_votes);
         comm->d_votes = nullptr;
         comm->votes_bytes = 0;
-        const char* inj = getenv("BA_TEST_VOTE_ENOMEM");  // test-only: inject the failure
-        if ((inj && inj[0] == '1') || hipMalloc(&comm->d_votes, need) != hipSuccess)
+        if (hipMalloc(&comm->d_votes, need) != hipSuccess)
             local = failf(BA_ENOMEM, "vote buffer (%zu B)", need);
         else
             comm->votes_bytes = need;
@@ -415,9 +552,8 @@ extern "C" int ba_run_instance_split_level_multi(struct ba_ctx* ctx, struct ba_c
     // allocate its vote buffer cannot join the grouped broadcasts (its peers
     // would wait in them forever), so every rank learns of any failure here
     // and all of them skip the exchange together.
-    int late = BA_OK;  // this rank's agreement read-back failed: join the exchange, report after
     {
-        const int rc_pre = preagree(comm, local, &late);
+        const int rc_pre = preagree(comm, local);
         if (rc_pre != BA_OK) return rc_pre;
     }
     if (local == BA_OK && batch > 0) {
@@ -438,7 +574,6 @@ extern "C" int ba_run_instance_split_level_multi(struct ba_ctx* ctx, struct ba_c
         local = ba_root_from_split_votes_device(ctx, p, batch, level, d_faulty_mask, d_order,
                                                 comm->d_votes, d_decisions, d_outcome, comm->d_cnt,
                                                 comm->stream);
-    if (local == BA_OK) local = late;
     return finish_job(comm, local, counters_out, false);
 }
 

@@ -836,15 +836,11 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM3W_MIN_BLOCKS(N)) void k_om3w(
     constexpr int L = G::L, C = G::C, W = G::W, NIN = G::NIN;
     constexpr uint32_t ME = 3;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)threadIdx.x) >> 6,
+                   wpb = blockDim.x >> 6;
     uint64_t* img = lds + (uint64_t)wv * G::words;
     const uint64_t total_words = (batch + 63) / 64;
     const uint64_t ntasks = (total_words + W - 1) / W;
-    // this lane's (word, leaf block) in the subtree rounds
-    const uint32_t lw_ = lane / C, la = lane - lw_ * C;
-    const bool act = lane < (uint32_t)G::LANES;
-    const uint32_t lw = act ? lw_ : 0;
-    const Om3LaneOffsets<N> lofs(la);
     uint64_t folded = 0;  // run counters folded per task (wave_fold)
     FUSED_STAMP_INIT();
 #ifdef BA_FUSED_STAMPS
@@ -855,6 +851,16 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM3W_MIN_BLOCKS(N)) void k_om3w(
     // third wave per SIMD for a second launch in flight)
     for (uint64_t task = (uint64_t)blockIdx.x * wpb + wv; task < ntasks;
          task += (uint64_t)gridDim.x * wpb) {
+        // every lane-derived value is formed per task from the lane index (mbcnt,
+        // no VGPR live across tasks): kept live across the task loop, they were
+        // the values the register allocator spilled around the prologue
+        uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        asm volatile("" : "+v"(lane));
+        // this lane's (word, leaf block) in the subtree rounds
+        const uint32_t lw_ = lane / C, la = lane - lw_ * C;
+        const bool act = lane < (uint32_t)G::LANES;
+        const uint32_t lw = act ? lw_ : 0;
+        const Om3LaneOffsets<N> lofs(la);
         const uint64_t w0 = task * W;
         const uint64_t gw0 = (first_trial >> 6) + w0;
         if constexpr (STAGED)
@@ -896,9 +902,9 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM3W_MIN_BLOCKS(N)) void k_om3w(
         __builtin_amdgcn_wave_barrier();
         FUSED_STAMP(4);
     }
-    wave_flush_folded(folded, lane, wv, wpb, counters, sk, (DIAG & 4) != 0);
+    wave_flush_folded(folded, threadIdx.x & 63, wv, wpb, counters, sk, (DIAG & 4) != 0);
 #ifdef BA_FUSED_STAMPS
-    if (lane == 0 && blockIdx.x * wpb + wv < (uint32_t)kPartialRows)
+    if ((threadIdx.x & 63) == 0 && blockIdx.x * wpb + wv < (uint32_t)kPartialRows)
     {
         for (int i = 0; i < 6; ++i) g_fused_stamps[blockIdx.x * wpb + wv][i] = st_acc[i];
         g_fused_stamps[blockIdx.x * wpb + wv][6] = rt0;
@@ -963,17 +969,11 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM4W_BLOCKS_PER_CU) void k_om4w(
     constexpr int NIN = G::NIN;
     constexpr uint32_t ME = 4;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)threadIdx.x) >> 6,
+                   wpb = blockDim.x >> 6;
     uint64_t* img = lds + (uint64_t)wv * G::words;
     const uint64_t total_words = (batch + 63) / 64;
     const uint64_t ntasks = (total_words + W - 1) / W;
-    const uint32_t lw_ = lane / C2, la = lane - lw_ * C2;
-    const bool act = lane < (uint32_t)G::LANES;
-    const uint32_t lw = act ? lw_ : 0;
-    // member a of lane la's leaf block is E2[a + (a >= la)]; member d's R3T row
-    // is d + (d >= la) (the k_om3w tables, E2 in place of E, C2 in place of C + 1)
-    const LaneBytes<S> mem([la](int a) { return 8u * (a + ((uint32_t)a >= la ? 1u : 0u)); });
-    const LaneBytes<S> r3o([la](int d) { return (uint32_t)d >= la ? 8u * C2 : 0u; });
     uint64_t folded = 0;  // run counters folded per task (wave_fold)
     // tasks: the first wave-round static, then (sk.tasks != nullptr: a persistent
     // launch) each further task from the launch's atomic counter, fetched at the
@@ -983,6 +983,16 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM4W_BLOCKS_PER_CU) void k_om4w(
     // one wave for the rest of the launch
     const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
     for (uint64_t task = (uint64_t)blockIdx.x * wpb + wv; task < ntasks;) {
+        // lane-derived values per task, from mbcnt (as k_om3w: none live across tasks)
+        uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        asm volatile("" : "+v"(lane));
+        const uint32_t lw_ = lane / C2, la = lane - lw_ * C2;
+        const bool act = lane < (uint32_t)G::LANES;
+        const uint32_t lw = act ? lw_ : 0;
+        // member a of lane la's leaf block is E2[a + (a >= la)]; member d's R3T row
+        // is d + (d >= la) (the k_om3w tables, E2 in place of E, C2 in place of C + 1)
+        const LaneBytes<S> mem([la](int a) { return 8u * (a + ((uint32_t)a >= la ? 1u : 0u)); });
+        const LaneBytes<S> r3o([la](int d) { return (uint32_t)d >= la ? 8u * C2 : 0u; });
         uint32_t next_raw = 0;
         if (sk.tasks != nullptr && lane == 0) next_raw = atomicAdd(sk.tasks, 1u);
         const uint64_t w0 = task * W;
@@ -1113,7 +1123,7 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM4W_BLOCKS_PER_CU) void k_om4w(
         __builtin_amdgcn_wave_barrier();
         task = sk.tasks != nullptr ? nwaves + __builtin_amdgcn_readfirstlane(next_raw) : task + nwaves;
     }
-    wave_flush_folded(folded, lane, wv, wpb, counters, sk, false);
+    wave_flush_folded(folded, threadIdx.x & 63, wv, wpb, counters, sk, false);
 }
 
 // WAVE engine launch: one wave per W-word task, 4 independent waves per block,

@@ -57,6 +57,8 @@ extern "C" {
 #define BA_EDEVICE (-3)    /* HIP runtime error / no device                     */
 #define BA_ENOTSUP (-4)    /* combination not supported (e.g. table mode, m>1)  */
 #define BA_ETOOBIG (-5)    /* tree too large for the requested engine          */
+#define BA_EABORTED (-6)   /* communicator aborted (watchdog timeout or a rank's  */
+                           /* transport failure): destroy it, create a new one  */
 
 /* lie source for faulty senders (ba.py:45, ba.py:269: random.randint(0,1)) */
 #define BA_LIE_PHILOX 0 /* Philox4x32-10 keyed by (seed; trial word, level, slot) */
@@ -274,6 +276,18 @@ int ba_comm_create(struct ba_ctx* ctx, int nranks, int rank,
                    const unsigned char id[BA_COMM_ID_BYTES], struct ba_comm** out);
 void ba_comm_destroy(struct ba_comm* comm);
 int ba_comm_rank(struct ba_comm* comm, int* nranks, int* rank);
+/* Watchdog of the blocking whole jobs below.  A job waits for its collectives
+ * by polling the comm's stream; past `timeout_ms` (default 300000, or
+ * BA_COMM_TIMEOUT_MS at ba_comm_create) it aborts the communicator
+ * (ncclCommAbort: this rank's collectives return) and fails with BA_EABORTED.
+ * That bounds every rank's wait when a peer left the protocol (a dead process,
+ * or a rank whose own transport failed and which aborted itself: it cannot
+ * tell its peers, RCCL has no such message, so they learn it from their own
+ * watchdog).  ba_comm_abort does the same on demand (e.g. from a host-side
+ * watchdog of the asynchronous collectives).  An aborted comm fails every
+ * further call with BA_EABORTED; ba_comm_destroy still frees it. */
+int ba_comm_set_timeout(struct ba_comm* comm, uint64_t timeout_ms);
+int ba_comm_abort(struct ba_comm* comm);
 
 /* Partition arithmetic (host only).  ba_trial_share: rank's contiguous,
  * 64-trial-word-aligned share [first, first + count) of total_trials, words

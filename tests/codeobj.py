@@ -126,3 +126,23 @@ def writelane_hazards(instrs: list, need: int = WRITELANE_WAIT_STATES) -> tuple:
                 break
             ws += _wait_states(instrs[j])
     return bad, checked
+
+
+def kernel_resources(lib_path: str = LIB) -> dict:
+    """{kernel symbol: {vgpr, sgpr, vgpr_spill, sgpr_spill}} from the AMDGPU metadata
+    notes of every gfx950 code object in the library."""
+    res = {}
+    for co in code_objects(lib_path):
+        with tempfile.NamedTemporaryFile(suffix=".co") as f:
+            f.write(co)
+            f.flush()
+            notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", f.name], check=True,
+                                   capture_output=True, text=True).stdout
+        for blk in notes.split("- .agpr_count")[1:]:
+            def field(key):
+                return int(re.search(rf"\.{key}:\s+(\d+)", blk).group(1))
+            name = re.search(r"\.name:\s+(\S+)", blk).group(1)
+            res[name] = {"vgpr": field("vgpr_count"), "sgpr": field("sgpr_count"),
+                         "vgpr_spill": field("vgpr_spill_count"),
+                         "sgpr_spill": field("sgpr_spill_count")}
+    return res

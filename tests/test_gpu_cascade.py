@@ -337,3 +337,73 @@ def test_cascade_fuzz_vs_oracle(engine, monkeypatch, i, n, m, B, mode, two, fani
     same(res.decisions, od, f"decisions case {i}")
     same(res.outcome, oo, f"outcome case {i}")
     assert {k: res.counters[k] for k in oc_} == oc_, i
+
+
+def test_cascade_chunk_capped_at_sink_capacity(engine):
+    """The counter sink takes < 2^16 units per replica (one unit = one word in
+    k_cascade, 64 replicas): a LEVELS call of 268.4M trials (64 x 65535 + 37 words,
+    more than one launch may carry) runs as two k_cascade chunks, its counters
+    add up (IC1 holds for every trial in bound), and the sink replicas are left
+    at zero -- the next small call is exact against the oracle."""
+    from ba_amd import lib as L
+    words = 64 * 65535 + 37
+    B = 64 * words
+    p = L.make_params(10, 3, 5, L.LIE_PHILOX, L.FAULTY_RANDOM, 3, L.ORDER_RANDOM, L.ATTACK,
+                      L.ENGINE_LEVELS, 0)
+    import torch
+    cnt = torch.zeros(16, dtype=torch.int64, device="cuda")
+    engine.profile(True)
+    engine.run_device(p, B, d_counters=cnt.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    prof = engine.profile_read()
+    engine.profile(False)
+    c = dict(zip(L.COUNTER_NAMES, cnt.cpu().tolist()))
+    assert prof["k_cascade"][0] == 2, prof
+    assert c["trials"] == B and c["agreement"] == B and c["in_bound"] == B
+    assert c["quorum_retreat"] + c["quorum_attack"] + c["quorum_undetermined"] == B
+    kw = dict(seed=6, faulty_mode=L.FAULTY_RANDOM, f=4, order_mode=L.ORDER_RANDOM)
+    _check(engine.run(10, 3, 700, engine=L.ENGINE_LEVELS, **kw), 10, 3, 700, **kw)
+
+
+def test_split_falls_back_to_levels_when_cascade_scratch_does_not_fit(monkeypatch):
+    """Range mode sizes the cascade's scratch for the whole tree per word; when
+    that does not fit the budget in one chunk, the split runs the per-range LEVELS
+    kernels (scratch shrinks with the rank's range) instead of failing with
+    ETOOBIG, and the root pass (k_cascade_wtop) grows no scratch at all.  At a
+    1 MiB budget, n=16, m=5, batch 1024: every second-hop unit's votes one unit at
+    a time, then the root pass, equal the oracle."""
+    import torch
+
+    from ba_amd import lib as L
+    monkeypatch.setenv("BA_SCRATCH_BYTES", str(1 << 20))
+    eng = L.Engine(0)
+    try:
+        n, m, B = 16, 5, 1024
+        kw = dict(seed=21, faulty_mode=L.FAULTY_RANDOM, f=5, order_mode=L.ORDER_RANDOM,
+                  first_trial=64)
+        p = L.make_params(n, m, **kw)
+        units, per, W = L.split_units(n, m, 2), n - 3, (B + 63) // 64
+        votes = torch.zeros((units * per, W), dtype=torch.int64, device="cuda")
+        s = torch.cuda.current_stream().cuda_stream
+        eng.profile(True)
+        for u in range(units):
+            eng.split_votes_device(p, B, 2, u, u + 1, votes[u * per:].data_ptr(), stream=s)
+        torch.cuda.synchronize()
+        prof = eng.profile_read()
+        eng.profile(False)
+        assert not any("k_cascade" in k for k in prof), prof  # the LEVELS kernels ran
+        dec = torch.empty(B, dtype=torch.int64, device="cuda")
+        out = torch.empty(B, dtype=torch.uint8, device="cuda")
+        cnt = torch.zeros(16, dtype=torch.int64, device="cuda")
+        scratch_before = eng.memory()["scratch"]
+        eng.root_from_split_votes_device(p, B, 2, votes.data_ptr(), cnt.data_ptr(),
+                                         d_decisions=dec.data_ptr(), d_outcome=out.data_ptr(),
+                                         stream=s)
+        torch.cuda.synchronize()
+        assert eng.memory()["scratch"] == scratch_before
+        od, oo, oc = oracle_c.sliced_run(n, m, B, **kw)
+        same(dec.cpu().numpy().view(np.uint64), od, "decisions")
+        same(out.cpu().numpy(), oo, "outcome")
+        assert cnt.cpu().tolist()[:12] == list(oc.values())
+    finally:
+        eng.close()

@@ -128,3 +128,39 @@ def test_writelane_check_catches_missing_nop(tmp_path):
         res[tag] = codeobj.writelane_hazards(ins)
     assert res["nop"][0] == [] and res["nop"][1] > 0
     assert len(res["nonop"][0]) > 0 and min(b[3] for b in res["nonop"][0]) < 2
+
+
+# VGPR spill budgets of the shipped kernels (scratch traffic: each spilled VGPR is
+# a 256-B store + load per wave where it is spilled).  The bench's kernel
+# k_om3w<10, staged> and every cascade kernel must not spill at all; the other
+# WAVE instantiations are held at what they compile to now (round 5: lane-derived
+# values formed per task from mbcnt, so none is live across the task loop).
+SPILL_BUDGET = [  # (symbol regex, max VGPR spills)
+    (r"_ZN2ba6k_om3wILi10ELi0ELb1E", 0),   # the bench kernel (BASELINE config 2)
+    (r"_ZN2ba6k_om3wILi9ELi0ELb1E", 1),
+    (r"_ZN2ba6k_om3w", 0),
+    (r"_ZN2ba6k_om4wILi13ELb1E", 3),      # config 3 (staged)
+    (r"_ZN2ba6k_om4wILi13ELb0E", 8),      # config 3 (inputs in-kernel)
+    (r"_ZN2ba6k_om4wILi1[01]ELb", 1),
+    (r"_ZN2ba6k_om4wILi12ELb", 29),
+    (r"_ZN2ba6k_om4wILi14ELb", 48),
+    (r"_ZN2ba6k_om4w", 0),
+    (r"_ZN2ba\d+k_cascade", 0),            # config 5 (units, fan-in, root pass)
+]
+
+
+def test_register_spill_budgets():
+    import re
+
+    import codeobj
+    res = codeobj.kernel_resources()
+    checked = 0
+    for name, r in res.items():
+        for pat, budget in SPILL_BUDGET:
+            if re.match(pat, name):
+                assert r["vgpr_spill"] <= budget, (name, r, budget)
+                checked += 1
+                break
+    bench = [r for n, r in res.items() if n.startswith("_ZN2ba6k_om3wILi10ELi0ELb1E")]
+    assert len(bench) == 1 and bench[0]["vgpr_spill"] == 0 and bench[0]["vgpr"] <= 168, bench
+    assert checked >= 60, checked

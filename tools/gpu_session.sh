@@ -10,6 +10,11 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 mkdir -p gpurun_out
 STAGES="${*:-tests smoke bench prof}"
+# heartbeat: a step that prints nothing for minutes (a multi-rank launch importing
+# torch on a fresh box) must not look hung
+(while true; do date +%T >> gpurun_out/heartbeat.txt; sleep 30; done) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 run() {  # name seconds cmd...
   local name=$1 t=$2; shift 2
   echo "[$(date +%T)] start $name" | tee -a gpurun_out/steps.log
@@ -61,6 +66,7 @@ for s in $STAGES; do
             run c5ab_1024_$t 300 env BA_HIP_LIB=$ROOT/$lib python -u tools/config5_prof.py --batch 1024 || exit $?
             run c5ab_1_$t 300 env BA_HIP_LIB=$ROOT/$lib python -u tools/config5_prof.py --batch 1 --reps 500 || exit $?
           done; done ;;
+    multirank) run pytest_multirank 900 python -u -m pytest tests/test_multirank_gpu.py tests/test_dist.py -m gpu -v --timeout 420 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
     casc) run pytest_casc 600 python -u -m pytest tests/test_gpu_cascade.py tests/test_dist.py -m gpu -v --timeout 200 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
     c5prof) for b in 1024 1; do
           (cd /tmp && export TMPDIR=/tmp && mkdir -p "$ROOT/gpurun_out/c5prof_$b" && \
