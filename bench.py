@@ -242,10 +242,11 @@ def run_cpu_baseline(n, m, seed, fmax, budget_s, ranges, gpu_counters, extra_fir
 def clock_from_probes(p0, p1):
     """Average engine clock between two ba_clock_probe_device probes, per XCD:
     (d s_memtime / d s_memrealtime) x 100 MHz, rows {xcc, hw, memtime, realtime}.
-    s_memtime is a per-shader-engine counter, so a difference is only taken between
-    rows of the SAME XCD, shader engine and CU (HW_ID bits 8-15: CU, SH, SE) in the
-    two probes; the XCD's clock is the median over those pairs.  An XCD whose probe
-    blocks landed on no common CU is left out (a difference across engines is not a
+    s_memtime is a per-CU counter (two CUs' counters differ by arbitrary offsets,
+    even within one shader engine: profiles/r04w_probe_pairing.log), so a difference
+    is only taken between rows of the SAME XCD and CU (HW_ID bits 8-15: CU, SH, SE)
+    in the two probes; the XCD's clock is the median over those pairs.  An XCD whose
+    probe blocks landed on no common CU is left out (a difference across CUs is not a
     clock).  Returns (median MHz over the XCDs measured, {xcc: MHz})."""
     import statistics
 

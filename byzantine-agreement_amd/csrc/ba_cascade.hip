@@ -48,9 +48,6 @@
 // form (Csa::ge_from, the WAVE kernels' default) took k_cascade<16,5> from 126
 // to 142 VGPRs (4 -> 3 waves per SIMD) for ~1% fewer instructions.
 #define BA_CSA_GE_RESOLVE 1
-#ifdef BA_CASCADE_SKEYS  // A/B: Philox round keys as SGPR operands in this TU
-#define BA_PHILOX_SKEYS 1
-#endif
 #include "ba_wave.hpp"
 #include "../../include/ba.h"  // BA_C_CHECK_MISMATCH
 
@@ -60,10 +57,7 @@ constexpr int kCascMaxLevels = 8;
 constexpr uint32_t kCascCounterStride = 32;  // uint32 per counter: one 128-B line each
 // waves per block (one-wave blocks, so that a wave taking fan-in steps holds
 // only its own slot, measured no faster: 70.6 vs 69.9 us, n=16 m=5 x 1024)
-#ifndef BA_CASC_WAVES
-#define BA_CASC_WAVES 4
-#endif
-constexpr uint32_t kCascWaves = BA_CASC_WAVES;
+constexpr uint32_t kCascWaves = 4;
 
 struct CascArgs {
     uint64_t seed;
@@ -410,22 +404,13 @@ __device__ __forceinline__ uint64_t relay_slots(const CascArgs& a, const uint64_
     return r;
 }
 
-// The arrival that completes a counter may take an agent-scope acquire before
-// the children are read (-DBA_CASC_ACQUIRE=1, A/B builds).  Off by default:
-// the acquire invalidates this CU's L1 and nothing else (MI355X_MICROARCH.md,
-// fence table), and every child load is an sc1 load, which bypasses L1; with
-// the child blocks padded to lines of their own no L2 holds a line of a
-// hand-off before its reader loads it.  Measured cost of the acquire: +4.1 us
-// per 1024-instance n=16 m=5 call, +1.3 us per single instance
+// No agent-scope acquire before the children are read: it would invalidate
+// this CU's L1 and nothing else (MI355X_MICROARCH.md, fence table), and every
+// child load is an sc1 load, which bypasses L1; with the child blocks padded to
+// lines of their own no L2 holds a line of a hand-off before its reader loads
+// it.  Measured cost of the acquire (round 4's A/B build): +4.1 us per
+// 1024-instance n=16 m=5 call, +1.3 us per single instance
 // (profiles/r04a_acquire_ab.log).
-#ifndef BA_CASC_ACQUIRE
-#define BA_CASC_ACQUIRE 0
-#endif
-__device__ __forceinline__ void casc_acquire() {
-#if BA_CASC_ACQUIRE
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
-}
 
 // R store of one hand-off word (+ its tag in CHECK builds): write-through
 template <int N, int ME, int k, bool CHECK>
@@ -509,7 +494,6 @@ __device__ __forceinline__ void casc_finish(const CascArgs& a, const uint64_t* i
         else
             c = a.cnt + (uint64_t)(a.cnt_off[C::Q] + w) * kCascCounterStride;
         if (arrive_last(c, up_fan, lane)) {
-            casc_acquire();
             casc_step<N, ME, q - 1, CHECK>(a, in, scr, lane, w, ps, gw, tc, mm);
         }
     } else {
@@ -569,14 +553,8 @@ __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in,
 // k_cascade_top does the fan-in; alone: the lab's units-only ablation), 4 =
 // arrivals but no steps (lab only, tools/casc_lab.py, BA_CASC_DIAG; wrong
 // results).  The one-launch product uses 0.
-// minimum blocks per CU of the units-only launch (DIAG 2): A/B builds set
-// -DBA_CASC_UNITS_MINB=k (k = 4: 128 VGPRs, 4 waves/SIMD, with spills)
-#ifndef BA_CASC_UNITS_MINB
-#define BA_CASC_UNITS_MINB 1
-#endif
-#define BA_CASC_MINB(n, me, diag) ((diag) == 2 ? BA_CASC_UNITS_MINB : 1)
 template <int N, int ME, int DIAG = 0, bool CHECK = false, bool LAT = false>
-__global__ __launch_bounds__(64 * kCascWaves, BA_CASC_MINB(N, ME, DIAG)) void k_cascade(CascArgs a) {
+__global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
     using C = Casc<N, ME>;
     using U = CascU<N, ME, LAT>;
     constexpr int L = C::L, S = C::S, G = C::G, GP = C::GP, GPW = U::GPW, NIN = C::NIN, Q = C::Q;
@@ -708,7 +686,6 @@ __global__ __launch_bounds__(64 * kCascWaves, BA_CASC_MINB(N, ME, DIAG)) void k_
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         uint64_t lastmask = (DIAG & 4) ? 0ull : __ballot(last);
-        if (lastmask) casc_acquire();
         while (lastmask) {  // wave-uniform: every lane runs each completed parent's step
             const uint32_t b = (uint32_t)__builtin_ctzll(lastmask);
             lastmask &= lastmask - 1;

@@ -47,19 +47,13 @@ __host__ __device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32
 // ---------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al., SC'11).  Each round is 2 x v_mad_u64_u32 +
 // 2 x xor3 (tools/philox_bench: 9.5e11 calls/s on one MI355X vs 7.8e11 with
-// 2-input xors).  The key is kernel-uniform; where its round keys live is a
-// build choice of philox10_n (same results on every path):
-//   default           groups of 2-4 calls: round keys AND the two multipliers as
-//                     VGPR operands (KeysV, philox10_n_vk; a VALU op with an SGPR
-//                     operand issues slower; VGPR multipliers:
-//                     +2.4% calls/s in tools/philox_bench, BA_PHILOX_MSGPR keeps
-//                     them in SGPRs), rounds 2-9 as one generated asm statement
-//                     (ba_philox_asm.hpp)
-//   BA_PHILOX_SKEYS   groups of 2-4 calls: round keys in SGPRs, rounds 0-1 in
-//                     C, rounds 2-9 as the asm statement
-//   G = 1 (and any    the generic round loop, keys in SGPRs, products pinned
-//   BA_PHILOX_C /     to v_mad_u64_u32 from round 2 (BA_PHILOX_C: plain C
-//   BA_PHILOX_ROUND_ASM build)  products; both switches are A/B builds only)
+// 2-input xors).  The key is kernel-uniform.  Groups of 2-4 interleaved calls
+// (philox10_n) take the round keys AND the two multipliers as VGPR operands
+// (KeysV: a VALU op with an SGPR operand issues slower; VGPR
+// multipliers +2.4% calls/s in tools/philox_bench), rounds 0-1 in C and rounds
+// 2-9 as one generated asm statement (ba_philox_asm.hpp).  A single call
+// (philox10, G = 1) is the round loop with its products pinned to
+// v_mad_u64_u32 from round 2.  Same results on every path.
 // ---------------------------------------------------------------------------
 struct P4 {
     uint32_t x, y, z, w;
@@ -76,27 +70,16 @@ __host__ __device__ __forceinline__ void static_for_h(F&& f) {
 }
 
 // The two 32x32 -> 64-bit products of Philox round I.  From round 2 on each
-// is pinned to one v_mad_u64_u32 (inline asm; BA_PHILOX_C=1 builds leave it to
-// the compiler).  Left alone, the compiler splits ~40 of a WAVE round's
+// is pinned to one v_mad_u64_u32 (inline asm).  Left alone, the compiler splits ~40 of a WAVE round's
 // products into v_mul_hi_u32 + v_mul_lo_u32 pairs; pinned, the n=10 WAVE
 // kernel runs ~3% faster (tools/om3_lab.hip A/B, same outputs).  Rounds 0-1
 // stay plain C so the compiler can still share and strength-reduce the
 // products common to a lane's calls (same level and word).
-__device__ __forceinline__ uint64_t mad_u64_u32_pinned(uint32_t x, uint32_t m) {
-    uint64_t r, cc;
-    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(cc) : "v"(x), "s"(m));
-    return r;
-}
-
 template <int I>
 __host__ __device__ __forceinline__ void philox_mul2(uint32_t x, uint32_t z, uint64_t& p0,
                                                      uint64_t& p1) {
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(BA_PHILOX_C)
+#if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (I >= 2) {
-#ifdef BA_MAD_SPLIT_ASM
-        p0 = mad_u64_u32_pinned(x, 0xD2511F53u);
-        p1 = mad_u64_u32_pinned(z, 0xCD9E8D57u);
-#else
         // Both products in one asm statement: the hazard recognizer puts one
         // conservative s_nop after every inline-asm VALU def (it cannot see that
         // a v_mad_u64_u32 is neither a trans op nor an op_sel/SDWA write), so a
@@ -106,7 +89,6 @@ __host__ __device__ __forceinline__ void philox_mul2(uint32_t x, uint32_t z, uin
         asm("v_mad_u64_u32 %0, %2, %3, %5, 0\n\tv_mad_u64_u32 %1, %2, %4, %6, 0"
             : "=&v"(p0), "=v"(p1), "=&s"(cc)
             : "v"(x), "v"(z), "s"(0xD2511F53u), "s"(0xCD9E8D57u));
-#endif
         return;
     }
 #endif
@@ -123,7 +105,7 @@ __host__ __device__ __forceinline__ void philox_mul2(uint32_t x, uint32_t z, uin
 template <int I, int G>
 __host__ __device__ __forceinline__ void philox_mul2_n(const P4 (&c)[G], uint64_t (&p0)[G],
                                                        uint64_t (&p1)[G]) {
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(BA_PHILOX_C) && !defined(BA_MAD_SPLIT_ASM)
+#if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (I >= 2 && G >= 2 && G <= 4) {
         uint64_t cc;
         constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
@@ -176,15 +158,6 @@ __host__ __device__ __forceinline__ P4 philox10(P4 c, uint32_t k0, uint32_t k1) 
 // source order interleaves the chains, so each v_mad_u64_u32 result is used G
 // instructions later instead of right away (left to itself the scheduler runs
 // the calls one after another and exposes the multiply latency).
-#if defined(__HIP_DEVICE_COMPILE__) && defined(BA_PHILOX_VKEYS)
-// lab: the round keys as VGPR operands of the xor3s (the compiler sees them as
-// divergent values, so it keeps them in VGPRs instead of SGPRs)
-__device__ __forceinline__ uint32_t as_vgpr(uint32_t k) {
-    uint32_t r;
-    asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(k));
-    return r;
-}
-#endif
 // The key schedule of one seed in VGPRs (kv0[i], kv1[i] = round i's keys): a
 // VALU op with an SGPR operand issues slower than one with VGPR operands only
 // (tools/valu_cost operands: v_bitop3 xor3 4.5 vs 2.7 cycles per wave64
@@ -192,9 +165,7 @@ __device__ __forceinline__ uint32_t as_vgpr(uint32_t k) {
 // asm keeps the (uniform) values in VGPRs.
 struct KeysV {
     uint32_t k0[10], k1[10];
-#ifndef BA_PHILOX_MSGPR
-    uint32_t m0, m1;  // the multipliers as VGPR operands too (BA_PHILOX_MSGPR: SGPRs, A/B)
-#endif
+    uint32_t m0, m1;  // the multipliers as VGPR operands too
     __device__ __forceinline__ explicit KeysV(uint64_t seed)
         : KeysV((uint32_t)seed, (uint32_t)(seed >> 32)) {}
     // the asm is not volatile: a pure function of the seed, so the compiler can
@@ -206,11 +177,9 @@ struct KeysV {
             k1[i] = b + (uint32_t)i * 0xBB67AE85u;
             asm("" : "+v"(k0[i]), "+v"(k1[i]));
         }
-#ifndef BA_PHILOX_MSGPR
         m0 = 0xD2511F53u;
         m1 = 0xCD9E8D57u;
         asm("" : "+v"(m0), "+v"(m1));
-#endif
     }
 };
 
@@ -244,11 +213,7 @@ __device__ __forceinline__ void philox10_n_vk(P4 (&c)[G], const KeysV& kv) {
             z[g] = c[g].z;
             w[g] = c[g].w;
         }
-#ifndef BA_PHILOX_MSGPR
         philox_r29_asm_vkm<G>(x, y, z, w, rk0, rk1, kv.m0, kv.m1);
-#else
-        philox_r29_asm_vk<G>(x, y, z, w, rk0, rk1);
-#endif
 #pragma unroll
         for (int g = 0; g < G; ++g) c[g] = P4{x[g], y[g], z[g], w[g]};
     } else {
@@ -270,55 +235,11 @@ __device__ __forceinline__ void philox10_n_vk(P4 (&c)[G], const KeysV& kv) {
 
 template <int G>
 __host__ __device__ __forceinline__ void philox10_n(P4 (&c)[G], uint32_t k0, uint32_t k1) {
-#if defined(__HIP_DEVICE_COMPILE__) && defined(BA_PHILOX_VKEYS)
-    k0 = as_vgpr(k0);
-    k1 = as_vgpr(k1);
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(BA_PHILOX_C) && !defined(BA_PHILOX_ROUND_ASM) && \
-    !defined(BA_PHILOX_SKEYS)
+#if defined(__HIP_DEVICE_COMPILE__)
     // round keys as VGPR operands (KeysV, hoisted by the compiler): Philox calls
     // 8.4e11 -> 9.6e11 per second at 2 waves/SIMD (tools/philox_bench)
     if constexpr (G >= 2 && G <= 4) {
         philox10_n_vk<G>(c, KeysV(k0, k1));
-        return;
-    }
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(BA_PHILOX_C) && !defined(BA_PHILOX_ROUND_ASM)
-    // rounds 0-1 in C (the compiler shares and strength-reduces the products a
-    // lane's calls have in common), rounds 2-9 as one asm statement
-    // (ba_philox_asm.hpp: one hazard s_nop per group instead of one per round)
-    if constexpr (G >= 2 && G <= 4) {
-        static_for_h<0, 2>([&](auto i) {
-            uint64_t p0[G], p1[G];
-            philox_mul2_n<i(), G>(c, p0, p1);
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                P4 n;
-                n.x = xor3_32((uint32_t)(p1[g] >> 32), c[g].y, k0);
-                n.y = (uint32_t)p1[g];
-                n.z = xor3_32((uint32_t)(p0[g] >> 32), c[g].w, k1);
-                n.w = (uint32_t)p0[g];
-                c[g] = n;
-            }
-            k0 += 0x9E3779B9u;
-            k1 += 0xBB67AE85u;
-        });
-        uint32_t rk0[8], rk1[8], x[G], y[G], z[G], w[G];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            rk0[i] = k0 + (uint32_t)i * 0x9E3779B9u;
-            rk1[i] = k1 + (uint32_t)i * 0xBB67AE85u;
-        }
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            x[g] = c[g].x;
-            y[g] = c[g].y;
-            z[g] = c[g].z;
-            w[g] = c[g].w;
-        }
-        philox_r29_asm<G>(x, y, z, w, rk0, rk1);
-#pragma unroll
-        for (int g = 0; g < G; ++g) c[g] = P4{x[g], y[g], z[g], w[g]};
         return;
     }
 #endif

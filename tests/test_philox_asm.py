@@ -34,8 +34,19 @@ def philox_rounds(c, k0, k1, r0, r1):
     return [x, y, z, w]
 
 
-def parse(G, name="philox_r29_asm"):
-    src = open(HDR).read()
+_LAB = []
+
+
+def lab_header() -> str:
+    """The generator's --lab output (all three variants; lab builds only)."""
+    if not _LAB:
+        _LAB.append(subprocess.run([sys.executable, GEN, "--lab"], capture_output=True, text=True,
+                                   check=True).stdout)
+    return _LAB[0]
+
+
+def parse(G, name="philox_r29_asm_vkm"):
+    src = open(HDR).read() if name == "philox_r29_asm_vkm" else lab_header()
     m = re.search(r"%s<%d>\(.*?asm volatile\((.*?)\);\n}" % (name, G), src, re.S)
     assert m, f"no G={G} specialisation"
     body = m.group(1)
@@ -100,7 +111,8 @@ def run_asm(lines, outs, ins, env):
     return out
 
 
-@pytest.mark.parametrize("name", ["philox_r29_asm", "philox_r29_asm_vk", "philox_r29_asm_vkm"])
+# the shipped variant (product header) and the --lab ones
+@pytest.mark.parametrize("name", ["philox_r29_asm_vkm", "philox_r29_asm", "philox_r29_asm_vk"])
 @pytest.mark.parametrize("G", [2, 3, 4])
 def test_generated_rounds_match_philox(G, name):
     lines, outs, ins = parse(G, name)
@@ -124,3 +136,6 @@ def test_generated_rounds_match_philox(G, name):
 def test_header_is_generated():
     out = subprocess.run([sys.executable, GEN], capture_output=True, text=True, check=True).stdout
     assert out == open(HDR).read(), "ba_philox_asm.hpp is stale: rerun tools/gen_philox_asm.py"
+    # the product header holds only the variant the kernels call
+    assert "philox_r29_asm_vkm<2>" in out and "philox_r29_asm<2>" not in out
+    assert "philox_r29_asm_vk<2>" not in out and "philox_r29_asm_vkm<2>" in lab_header()

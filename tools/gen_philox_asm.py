@@ -25,6 +25,12 @@ Order per round: the 2G products, then the 2G xor3s, so each product is read
 schedule of philox_mul2_n).
 
 usage: python3 tools/gen_philox_asm.py > byzantine-agreement_amd/csrc/ba_philox_asm.hpp
+       python3 tools/gen_philox_asm.py --lab > <lab header>   (lab builds only)
+
+The product header holds only the variant the kernels use: round keys and
+multipliers as VGPR operands (philox_r29_asm_vkm).  --lab also emits the
+SGPR-key (philox_r29_asm) and SGPR-multiplier (philox_r29_asm_vk) variants
+that round 3/4's A/B runs measured -- for lab harnesses.
 """
 
 BASE = 0  # first fixed VGPR
@@ -164,36 +170,41 @@ __device__ __forceinline__ void {fname}<{G}>(uint32_t (&x)[{G}], uint32_t (&y)[{
 
 
 def main():
-    out = ['// GENERATED by tools/gen_philox_asm.py -- do not edit by hand.',
+    import sys
+    lab = "--lab" in sys.argv[1:]
+    out = ['// GENERATED by tools/gen_philox_asm.py' + (' --lab' if lab else '') + ' -- do not edit by hand.',
            '// Philox4x32-10 rounds 2..9 of G interleaved calls in one asm statement',
            '// (why and how: the generator\'s docstring).  Included by ba_device.hpp.',
            '#pragma once',
            '#include <stdint.h>',
            '',
            'namespace ba {',
-           '',
-           'template <int G>',
-           '__device__ __forceinline__ void philox_r29_asm(uint32_t (&x)[G], uint32_t (&y)[G],',
-           '                                               uint32_t (&z)[G], uint32_t (&w)[G],',
-           '                                               const uint32_t (&k0)[8], const uint32_t (&k1)[8]);',
-           '// the same with the round keys as VGPR operands (VALU ops with an SGPR operand',
-           '// issue slower: tools/valu_cost operands)',
-           'template <int G>',
-           '__device__ __forceinline__ void philox_r29_asm_vk(uint32_t (&x)[G], uint32_t (&y)[G],',
-           '                                                  uint32_t (&z)[G], uint32_t (&w)[G],',
-           '                                                  const uint32_t (&k0)[8], const uint32_t (&k1)[8]);',
-           '// the same with the multipliers as VGPR operands as well',
-           'template <int G>',
-           '__device__ __forceinline__ void philox_r29_asm_vkm(uint32_t (&x)[G], uint32_t (&y)[G],',
-           '                                                   uint32_t (&z)[G], uint32_t (&w)[G],',
-           '                                                   const uint32_t (&k0)[8], const uint32_t (&k1)[8],',
-           '                                                   uint32_t m0, uint32_t m1);',
            '']
+    if lab:
+        out += ['template <int G>',
+                '__device__ __forceinline__ void philox_r29_asm(uint32_t (&x)[G], uint32_t (&y)[G],',
+                '                                               uint32_t (&z)[G], uint32_t (&w)[G],',
+                '                                               const uint32_t (&k0)[8], const uint32_t (&k1)[8]);',
+                '// the same with the round keys as VGPR operands (VALU ops with an SGPR operand',
+                '// issue slower: tools/valu_cost operands)',
+                'template <int G>',
+                '__device__ __forceinline__ void philox_r29_asm_vk(uint32_t (&x)[G], uint32_t (&y)[G],',
+                '                                                  uint32_t (&z)[G], uint32_t (&w)[G],',
+                '                                                  const uint32_t (&k0)[8], const uint32_t (&k1)[8]);']
+    out += ['// round keys and multipliers as VGPR operands (VALU ops with an SGPR operand',
+            '// issue slower: tools/valu_cost operands)',
+            'template <int G>',
+            '__device__ __forceinline__ void philox_r29_asm_vkm(uint32_t (&x)[G], uint32_t (&y)[G],',
+            '                                                   uint32_t (&z)[G], uint32_t (&w)[G],',
+            '                                                   const uint32_t (&k0)[8], const uint32_t (&k1)[8],',
+            '                                                   uint32_t m0, uint32_t m1);',
+            '']
     out.append('#ifdef __HIP_DEVICE_COMPILE__  // device code only (host passes never call it)')
-    for G in (2, 3, 4):
-        out.append(gen(G))
-    for G in (2, 3, 4):
-        out.append(gen(G, "v"))
+    if lab:
+        for G in (2, 3, 4):
+            out.append(gen(G))
+        for G in (2, 3, 4):
+            out.append(gen(G, "v"))
     for G in (2, 3, 4):
         out.append(gen(G, "v", "v"))
     out.append('#endif')
