@@ -122,3 +122,29 @@ def test_config5_full_batch_vs_oracle(engine):
         comm.close()
     check(dec.cpu().numpy().view(np.uint64), out.cpu().numpy(), cnt, od, oo, ocnt,
           "config 5 first-hop split")
+
+
+@pytest.mark.parametrize("n", [4, 10])
+def test_config1_table_mode_1m_trials_vs_oracle(engine, n):
+    """ba.py-exact mode at batch scale (tools/run_configs.py --only 1): 1,048,576
+    OM(1) rounds, each its own random.seed(seed_t) and coins in ba.py's draw order
+    (ba_mt_table, the C++ MT19937 replay pinned on ba.py's 400 fixture rounds),
+    random faulty sets (commander included, beyond the bound too), random
+    stale-primary polls (ba.py:171) and orders (attack / retreat / other):
+    k_table's decisions, outcome bytes and counters equal the oracle's table mode
+    (the recursion of ba.py:159-195 fed the same coins)."""
+    from ba_amd import lib as L
+    T = 1 << 20
+    rng = np.random.default_rng(77 + n)
+    seeds = rng.integers(0, 1 << 63, T, dtype=np.uint64)
+    faulty = rng.integers(0, 1 << n, T).astype(np.uint32)
+    faulty[rng.random(T) < 0.5] &= 0  # half the trials loyal throughout
+    poll = (rng.integers(0, 1 << n, T) & ~1).astype(np.uint32)
+    order = rng.choice(np.array([0, 1, 2], np.uint8), T, p=[0.45, 0.45, 0.1])
+    tab, _ = L.mt_table(n, 1, seeds, faulty, poll, threads=host_threads())
+    res = engine.run(n, 1, T, lie_mode=L.LIE_TABLE, faulty=faulty, order=order, table=tab,
+                     poll=poll)
+    od, oo, ocnt = oracle_c.run(n, 1, T, lie_mode=1, faulty=faulty, order=order, table=tab,
+                                poll=poll, threads=host_threads())
+    check(res.decisions, res.outcome, res.counters, od, oo, ocnt, f"table mode n={n}")
+    assert ocnt["trials"] == T and 0 < ocnt["bound_violations"] < T

@@ -1,9 +1,17 @@
-"""BASELINE.json configs 3-5 (the non-headline ones) through the C ABI's
-multi-GPU entries (ba_run_trials_multi, ba_run_instance_split_multi; ba_amd.dist
-does the rendezvous).
+"""BASELINE.json configs 1 and 3-5 (the non-headline ones) through the C ABI
+(configs 3-5 through its multi-GPU entries, ba_run_trials_multi and
+ba_run_instance_split_multi; ba_amd.dist does the rendezvous).
 
-    python tools/run_configs.py [--only 3,4,5]                       # one GPU
+    python tools/run_configs.py [--only 1,3,4,5]                      # one GPU
     python -m torch.distributed.run --nproc-per-node N tools/run_configs.py  # N GPUs
+
+  1  ba.py-exact mode at batch scale: OM(1) at n=4 and n=10, 1M trials, each
+     trial its own ba.py round -- random.seed(seed_t), then the round's coins in
+     ba.py's draw order (ba.py:45, 269) -- with random faulty sets, stale-primary
+     polls (ba.py:171) and orders.  ba_mt_table (C++, every host thread) builds the
+     coin table; k_table (ba_run_trials_device, BA_LIE_TABLE) resolves the trials
+     from it on the device.  The kernel's rate and the table's generation time are
+     reported separately (one GPU, rank 0 only).
 
   3  n=13, m=4, 64M trials, trial-DP across ranks (counters all-reduced)
   4  n=10, m=3 faulty-count sweep f = 0..n/3+1, exactly f faulty, 1M trials each:
@@ -57,6 +65,7 @@ def counters(t):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="3,4,5")
+    ap.add_argument("--trials1", type=int, default=1 << 20)
     ap.add_argument("--trials3", type=int, default=64 << 20)
     ap.add_argument("--trials4", type=int, default=1 << 20)
     ap.add_argument("--batch5", type=int, default=1024)
@@ -74,6 +83,74 @@ def main():
     eng = L.Engine(local)
     comm = D.init_comm(eng)  # a one-rank communicator on one GPU
     out = []
+
+    if 1 in which and rank == 0:
+        import numpy as np
+        for n in (4, 10):
+            T = a.trials1
+            rng = np.random.default_rng(1000 + n)
+            seeds = np.arange(T, dtype=np.uint64) + np.uint64(n << 32)
+            # faulty sets: k ~ U{0..f_max+1} generals (the commander included) chosen
+            # uniformly, so some trials exceed the OM(1) bound
+            fmax = (n - 1) // 3 + 1
+            k = rng.integers(0, fmax + 1, T)
+            order_g = np.argsort(rng.random((T, n)), axis=1)
+            faulty = np.zeros(T, np.uint32)
+            for j in range(fmax):
+                faulty |= np.where(k > j, np.uint32(1) << order_g[:, j].astype(np.uint32), 0).astype(np.uint32)
+            poll = (rng.integers(0, 1 << n, T) & ~1).astype(np.uint32)  # stale primaries
+            order = rng.choice(np.array([0, 1, 2], np.uint8), T, p=[0.45, 0.45, 0.1])
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+            t0 = time.perf_counter()
+            tab, _ = L.mt_table(n, 1, seeds, faulty, poll, threads=threads)
+            t_tab = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            d_tab = torch.from_numpy(tab.view(np.int32)).to(dev)
+            d_f = torch.from_numpy(faulty.view(np.int32)).to(dev)
+            d_p = torch.from_numpy(poll.view(np.int32)).to(dev)
+            d_o = torch.from_numpy(order).to(dev)
+            torch.cuda.synchronize(dev)
+            t_h2d = time.perf_counter() - t0
+            dec = torch.empty(T, dtype=torch.int64, device=dev)
+            outc = torch.empty(T, dtype=torch.uint8, device=dev)
+            cnt = torch.zeros(16, dtype=torch.int64, device=dev)
+            p = L.make_params(n, 1, 0, L.LIE_TABLE, L.FAULTY_GIVEN, 0, L.ORDER_GIVEN, L.ATTACK,
+                              L.ENGINE_AUTO, 0, tab.shape[1])
+            st = torch.cuda.Stream(dev)
+
+            def call1():
+                eng.run_device(p, T, d_faulty=d_f.data_ptr(), d_order=d_o.data_ptr(),
+                               d_table=d_tab.data_ptr(), d_poll=d_p.data_ptr(),
+                               d_decisions=dec.data_ptr(), d_outcome=outc.data_ptr(),
+                               d_counters=cnt.data_ptr(), stream=st.cuda_stream)
+            call1()
+            torch.cuda.synchronize(dev)
+            first = counters(cnt)
+            reps = 20
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            cnt.zero_()
+            torch.cuda.synchronize(dev)
+            e0.record(st)
+            for _ in range(reps):
+                call1()
+            e1.record(st)
+            torch.cuda.synchronize(dev)
+            ms = e0.elapsed_time(e1) / reps
+            if any(v != first[c] * reps for c, v in counters(cnt).items()):
+                raise SystemExit("config 1: repeated calls disagree")
+            out.append({"config": 1, "workload": f"ba.py OM(1) bit-exact, n={n}, {T} trials, one "
+                        "MT19937 seed per trial (random.seed + the round's coins in ba.py's draw "
+                        "order), random faulty sets / stale-primary polls / orders",
+                        "n": n, "m": 1, "trials": T,
+                        "kernel_trial_decisions_per_s": T / (ms * 1e-3), "kernel_ms_per_call": ms,
+                        "kernel_timing": "HIP events over 20 back-to-back k_table calls on one "
+                                         "stream, table and inputs resident in HBM",
+                        "table_generation_s": t_tab, "table_generation_trials_per_s": T / t_tab,
+                        "table_threads": threads or os.cpu_count(),
+                        "table_bytes": int(tab.nbytes), "h2d_s": t_h2d,
+                        "end_to_end_trials_per_s": T / (t_tab + t_h2d + ms * 1e-3),
+                        "n_gpus": 1, "counters": first})
+            del d_tab, d_f, d_p, d_o, dec, outc
 
     if 3 in which:
         n, m, T = 13, 4, a.trials3
