@@ -43,7 +43,8 @@ EXPORTS = ["ba_version", "ba_device_count", "ba_ctx_create", "ba_ctx_destroy", "
            "ba_run_instance_split_multi", "ba_split_units", "ba_split_vote_slots",
            "ba_split_share", "ba_split_votes_device", "ba_root_from_split_votes_device",
            "ba_comm_allgather_split_votes_device", "ba_run_instance_split_level_multi",
-           "ba_clock_probe_device", "ba_ctx_memory", "ba_comm_set_timeout", "ba_comm_abort"]
+           "ba_clock_probe_device", "ba_ctx_memory", "ba_comm_set_timeout", "ba_comm_abort",
+           "ba_mt_table_device"]
 PROBE_BLOCKS = 2048  # BA_PROBE_BLOCKS
 
 
@@ -121,6 +122,8 @@ def load(path: str | None = None):
     lib.ba_om1_coin_count.restype = u32
     lib.ba_mt_draw_coins.argtypes = [ctypes.POINTER(MTState), u32, vp, u32]
     lib.ba_mt_table.argtypes = [u32, u32, u64, vp, vp, vp, u32, vp, vp, i32]
+    if hasattr(lib, "ba_mt_table_device"):  # (A/B runs may load an older library)
+        lib.ba_mt_table_device.argtypes = [vp, u32, u32, u64, vp, vp, vp, u32, vp, vp, vp]
     lib.ba_vote_slots.argtypes = [u32, u32, u32, u32]
     lib.ba_vote_slots.restype = u64
     lib.ba_subtree_votes_device.argtypes = [vp, ctypes.POINTER(Params), u64, u32, u32, vp, vp, vp,
@@ -140,8 +143,9 @@ def load(path: str | None = None):
                                         ctypes.POINTER(Counters), ctypes.POINTER(u64),
                                         ctypes.POINTER(u64)]
     lib.ba_comm_rank.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
-    lib.ba_comm_set_timeout.argtypes = [vp, u64]
-    lib.ba_comm_abort.argtypes = [vp]
+    if hasattr(lib, "ba_comm_abort"):
+        lib.ba_comm_set_timeout.argtypes = [vp, u64]
+        lib.ba_comm_abort.argtypes = [vp]
     lib.ba_subtree_share.argtypes = [u32, i32, i32, ctypes.POINTER(u32), ctypes.POINTER(u32)]
     lib.ba_comm_allreduce_device.argtypes = [vp, vp, vp]
     lib.ba_comm_allgather_votes_device.argtypes = [vp, u32, u32, u64, vp, vp]
@@ -305,6 +309,14 @@ class Engine:
         _check(self.lib, self.lib.ba_ctx_memory(self.handle, ctypes.byref(sc), ctypes.byref(cn),
                                                 ctypes.byref(bu)))
         return {"scratch": sc.value, "counters": cn.value, "budget": bu.value}
+
+    def mt_table_device(self, n: int, m: int, batch: int, d_seeds: int, d_faulty: int, stride: int,
+                        d_table: int, d_poll=0, d_next_word=0, stream=0):
+        """ba.py's coin table on the device (ba_mt_table_device): row t = the coins of
+        random.seed(seeds[t]) + one round over (faulty[t], poll[t]); asynchronous."""
+        _check(self.lib, self.lib.ba_mt_table_device(self.handle, n, m, batch, d_seeds, d_faulty,
+                                                     d_poll or None, stride, d_table,
+                                                     d_next_word or None, stream or None))
 
     def clock_probe_device(self, d_out: int, stream=0):
         """Enqueue the engine-clock probe (ba_clock_probe_device): PROBE_BLOCKS rows of

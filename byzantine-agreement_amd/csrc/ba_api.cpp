@@ -851,6 +851,43 @@ static int ordered(ba_ctx* ctx, void* stream, F&& body) {
     return rc;
 }
 
+// ba.py's coin table on the device: ba_mt_table's rows (random.seed(seed_t), then
+// one round's coins in ba.py's draw order, ba.py:45, 269), chunked so the
+// generators' states ([624][chunk] uint32, ba_mtdev.hip) fit the scratch budget.
+extern "C" int ba_mt_table_device(ba_ctx* ctx, uint32_t n, uint32_t m, uint64_t batch,
+                                  const uint64_t* d_seeds, const uint32_t* d_faulty_mask,
+                                  const uint32_t* d_poll_commander, uint32_t stride,
+                                  uint32_t* d_table, uint32_t* d_next_word, void* stream) {
+    if (!ctx) return fail(BA_EINVAL, "ctx is NULL");
+    if (n < 1 || n > BA_MAX_GENERALS) return fail(BA_EINVAL, "n=%u outside 1..%d", n, BA_MAX_GENERALS);
+    const uint64_t L = n - 1;
+    if ((uint64_t)stride * 32 < L + L * L)
+        return fail(BA_EINVAL, "stride %u words < %llu coins of an n=%u round", stride,
+                    (unsigned long long)(L + L * L), n);
+    if (batch && (!d_seeds || !d_faulty_mask || !d_table))
+        return fail(BA_EINVAL, "d_seeds, d_faulty_mask and d_table are required");
+    if (batch == 0) return BA_OK;
+    return ordered(ctx, stream, [&] {
+        const hipStream_t s = (hipStream_t)stream;
+        const uint64_t per = mt_table_state_bytes_per_trial();
+        uint64_t chunk = ctx->scratch_budget / per;
+        if (chunk > batch) chunk = batch;
+        if (chunk > (1ull << 31)) chunk = 1ull << 31;
+        if (chunk == 0) return fail(BA_ETOOBIG, "scratch budget %zu < %llu B", ctx->scratch_budget,
+                                    (unsigned long long)per);
+        int rc;
+        if ((rc = ctx->scratch.grow(chunk * per)) != BA_OK) return rc;
+        for (uint64_t c0 = 0; c0 < batch; c0 += chunk) {
+            const uint64_t T = batch - c0 < chunk ? batch - c0 : chunk;
+            HIP_TRY(launch_mt_table(n, m, T, d_seeds + c0, d_faulty_mask + c0,
+                                    d_poll_commander ? d_poll_commander + c0 : nullptr, stride,
+                                    d_table + c0 * stride, d_next_word ? d_next_word + c0 : nullptr,
+                                    (uint32_t*)ctx->scratch.p, s, &ctx->prof));
+        }
+        return BA_OK;
+    });
+}
+
 extern "C" int ba_run_trials_device(ba_ctx* ctx, const ba_params* p, uint64_t batch,
                                     const uint32_t* d_faulty, const uint8_t* d_order,
                                     const uint32_t* d_table, const uint32_t* d_poll,

@@ -53,6 +53,30 @@
 
 namespace ba {
 
+// Lab builds only (tools/casc_stamps.sh compiles this file with
+// -DBA_CASC_STAMPS into a separate library): every wave of the units launch
+// records s_memtime at its phase boundaries, its HW_ID / XCC_ID and
+// s_memrealtime at entry and exit, read back by ba_lab_casc_stamps_read.  The
+// product build compiles none of it.
+#ifdef BA_CASC_STAMPS
+constexpr uint32_t kStampWaves = 1u << 16, kStampWords = 12;
+extern "C" __device__ unsigned long long ba_lab_casc_stamps[kStampWaves][kStampWords];
+__device__ unsigned long long ba_lab_casc_stamps[kStampWaves][kStampWords];
+#define CASC_STAMP(i) (st_[i] = __builtin_amdgcn_s_memtime())
+// k_cascade_mtop's wave 0 (and the root step it may take): one row per block
+extern "C" __device__ unsigned long long ba_lab_mtop_stamps[kStampWaves][16];
+__device__ unsigned long long ba_lab_mtop_stamps[kStampWaves][16];
+#define CASC_MSTAMP(i)                                                                   \
+    do {                                                                                 \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < kStampWaves)                         \
+            ba_lab_mtop_stamps[blockIdx.x][i] = (i) >= 14 ? __builtin_amdgcn_s_memrealtime() \
+                                                          : __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define CASC_STAMP(i) ((void)0)
+#define CASC_MSTAMP(i) ((void)0)
+#endif
+
 constexpr int kCascMaxLevels = 8;
 constexpr uint32_t kCascCounterStride = 32;  // uint32 per counter: one 128-B line each
 // waves per block (one-wave blocks, so that a wave taking fan-in steps holds
@@ -104,7 +128,12 @@ constexpr uint32_t casc_sz(int L, int k) {
 constexpr uint32_t casc_grp(int L, int k) { return (uint32_t)((L - k + 1) * (L - k)); }
 constexpr uint32_t casc_pad(int L, int k) { return (casc_grp(L, k) + 15u) & ~15u; }
 constexpr uint32_t casc_ngrp(int L, int k) { return k >= 2 ? casc_sz(L, k - 2) : 1u; }
-constexpr uint64_t casc_level_words(int L, int k) { return (uint64_t)casc_ngrp(L, k) * casc_pad(L, k); }
+// R_1 (the hand-off into the roots) is stored as granules: two 8-byte {value
+// half, epoch tag} words per value (casc_put / casc_kids), so its level takes
+// twice the words
+constexpr uint64_t casc_level_words(int L, int k) {
+    return (uint64_t)casc_ngrp(L, k) * casc_pad(L, k) * (k == 1 ? 2u : 1u);
+}
 
 template <int N, int ME>
 struct Casc {
@@ -412,13 +441,32 @@ __device__ __forceinline__ uint64_t relay_slots(const CascArgs& a, const uint64_
 // 1024-instance n=16 m=5 call, +1.3 us per single instance
 // (profiles/r04a_acquire_ab.log).
 
-// R store of one hand-off word (+ its tag in CHECK builds): write-through
+// R_1 granules (MI355X_MICROARCH.md's R2 form, cdna_hip_programming.md
+// Guideline 16): each 32-bit half of an R_1 word travels with the launch's
+// 32-bit tag in ONE aligned 8-byte sc1 store, so the data is its own flag: the
+// producer does not drain before its arrival, and the consumer (the step that
+// completes the word's root counter) re-reads every granule until all carry
+// the tag -- bounded: the stores were issued before the arrivals that let the
+// consumer in.  The consumer then zeroes the granules it read, so a replayed
+// launch (a captured graph repeats its epoch argument) never sees an old tag;
+// the tag is never 0.
+constexpr uint32_t kGranuleSpinCap = 1u << 16;  // s_sleep 1 polls before giving up (~ms)
+__device__ __forceinline__ uint32_t casc_gtag(uint64_t epoch) { return ((uint32_t)epoch << 1) | 1u; }
+
+// R store of one hand-off word (+ its tag in CHECK builds): write-through;
+// level 1 as two granules
 template <int N, int ME, int k, bool CHECK>
 __device__ __forceinline__ void casc_put(const CascArgs& a, uint32_t w, uint32_t x, uint64_t v,
                                          bool stale = false) {
     const uint64_t i = Casc<N, ME>::template addr<k>(w, x);
-    store_sc1(a.R[k] + i, v);
-    if constexpr (CHECK) store_sc1(a.tag[k] + i, casc_tag(stale ? a.epoch - 1 : a.epoch));
+    if constexpr (k == 1) {
+        const uint64_t tag = (uint64_t)casc_gtag(stale ? a.epoch - 1 : a.epoch) << 32;
+        store_sc1(a.R[1] + 2 * i, tag | (uint32_t)v);
+        store_sc1(a.R[1] + 2 * i + 1, tag | (uint32_t)(v >> 32));
+    } else {
+        store_sc1(a.R[k] + i, v);
+        if constexpr (CHECK) store_sc1(a.tag[k] + i, casc_tag(stale ? a.epoch - 1 : a.epoch));
+    }
 }
 
 // Step q for sigma (level q-1 slot s; q = 0: the word's roots), run by one
@@ -439,6 +487,7 @@ __device__ __forceinline__ void casc_kids(const CascArgs& a, uint32_t lane, uint
     constexpr int L = C::L, K = L - q;
     const bool act = lane < (uint32_t)K;
     const uint32_t r = act ? lane : 0u;
+    static_assert(q > 0 || VIN, "the roots read R_1 granules: casc_root_step");
     static_for<0, K - 1>([&](auto jj) {
         const uint32_t j = (uint32_t)jj() + ((uint32_t)jj() >= r ? 1u : 0u);
         const uint32_t x = (s * (uint32_t)K + j) * (uint32_t)(K - 1) + r - (r > j ? 1u : 0u);
@@ -459,6 +508,121 @@ __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in,
                                           uint32_t lane, uint32_t w, uint32_t s, uint64_t gw,
                                           TrialCounts& tc, uint32_t& mm);
 
+// The word's per-lane run counts of a one-word epilogue (wave_epilogue, W = 1:
+// only lanes 0..7, one byte of trials each, hold counts) to lane c = counter c:
+// an 8-lane sum by DPP (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror: three
+// VALU adds per counter, where 64-lane __shfl_xor sums took six LDS permutes in a
+// row -- ~1 us on the tail of a one-instance call), then lane 0's totals spread.
+__device__ __forceinline__ uint64_t word_counts_to_lanes(const TrialCounts& tw, uint32_t lane) {
+    uint64_t mine = 0;
+#pragma unroll
+    for (int c = 0; c < C_NUM; ++c) {
+        uint32_t x = tw.v[c];
+        x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+        x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
+        x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+        if (lane == (uint32_t)c) mine = tot;
+    }
+    return mine;
+}
+
+// The roots of word w from L_0 (lq) and the level-1 results cv: strict
+// majority attacks, a tie is undefined (ba.py:188-195); the quorum epilogue
+// (ba.py:197-255) and the word's counts into the counter sink.
+template <int N, int ME>
+__device__ __forceinline__ void casc_roots(const CascArgs& a, const uint64_t* in, uint64_t* scr,
+                                           uint32_t lane, uint32_t w, uint64_t lq,
+                                           const uint64_t (&cv)[N - 2]) {
+    using C = Casc<N, ME>;
+    constexpr int L = C::L, K = L, NIN = C::NIN;
+    const bool act = lane < (uint32_t)K;
+    const uint32_t r = act ? lane : 0u;
+    Csa<planes_c(K)> cnt;
+    cnt.template add<0>(lq);
+    static_for<0, K - 1>([&](auto jj) { cnt.template add<jj() + 1>(cv[jj()]); });
+    const uint64_t att = cnt.template ge<K, K / 2 + 1>();
+    const uint64_t tie = (K % 2 == 0) ? (cnt.template ge<K, K / 2>() & ~att) : 0ull;
+    // the epilogue overwrites bytes of its input planes: a private copy
+    if (lane < (uint32_t)NIN) scr[lane] = in[lane];
+    if (act) {
+        scr[NIN + r] = att;
+        scr[NIN + L + r] = tie;
+    }
+    __builtin_amdgcn_wave_barrier();
+    TrialCounts tw;
+    wave_epilogue<N, 1, (uint32_t)ME, 0>(scr, scr + NIN, lane, w, a.ntrials, a.decisions, a.outcome, tw);
+    __builtin_amdgcn_wave_barrier();
+    CASC_MSTAMP(10);
+    // the word's counts, straight into the sink: every word's root step runs
+    // exactly once per launch, so the word is the sink's unit and no block
+    // barrier is needed to combine waves (a wave exits as soon as it is done)
+    const uint64_t mine = word_counts_to_lanes(tw, lane);
+    if (a.counters) sink_counters(lane, mine, w, a.W, a.counters, a.sk);
+    CASC_MSTAMP(11);
+}
+
+// The root step of word w in a launch that handed R_1 off (the last arrival at
+// the word's root counter): the R_1 granules' loads go out first, L_0 is relayed
+// while they land, then every granule's tag is checked -- re-read (bounded)
+// until all are this launch's -- and the granules are zeroed for the next launch
+// (each has exactly one reader: receiver r of its slot).
+template <int N, int ME, bool CHECK>
+__device__ __forceinline__ void casc_root_step(const CascArgs& a, const uint64_t* in, uint64_t* scr,
+                                               uint32_t lane, uint32_t w, uint64_t gw, uint32_t& mm) {
+    using C = Casc<N, ME>;
+    constexpr int L = C::L, K = L;
+    const bool act = lane < (uint32_t)K;
+    const uint32_t r = act ? lane : 0u;
+    const uint32_t tag = casc_gtag(a.epoch);
+    uint64_t* gp[K - 1];
+    uint64_t g0[K - 1], g1[K - 1];
+    static_for<0, K - 1>([&](auto jj) {
+        const uint32_t j = (uint32_t)jj() + ((uint32_t)jj() >= r ? 1u : 0u);
+        gp[jj()] = a.R[1] + 2 * C::template addr<1>(w, j * (uint32_t)(K - 1) + r - (r > j ? 1u : 0u));
+        g0[jj()] = act ? load_sc1(gp[jj()]) : 0ull;
+        g1[jj()] = act ? load_sc1(gp[jj()] + 1) : 0ull;
+    });
+    uint32_t path[1];
+    const uint64_t lq = relay_slots<N, 0, K, 64>(a, in, scr, lane, true, 0u, 0u, path, gw);
+    CASC_MSTAMP(9);
+    auto fresh = [&]() {
+        bool ok = true;
+        static_for<0, K - 1>([&](auto jj) {
+            ok &= !act || ((uint32_t)(g0[jj()] >> 32) == tag && (uint32_t)(g1[jj()] >> 32) == tag);
+        });
+        return ok;
+    };
+    bool ok = fresh();
+    for (uint32_t spin = 0; !__all(ok) && spin < kGranuleSpinCap; ++spin) {  // wave-uniform
+        __builtin_amdgcn_s_sleep(1);
+        static_for<0, K - 1>([&](auto jj) {
+            g0[jj()] = act ? load_sc1(gp[jj()]) : 0ull;
+            g1[jj()] = act ? load_sc1(gp[jj()] + 1) : 0ull;
+        });
+        ok = fresh();
+    }
+    // a granule still stale at the cap: never in a correct run.  Counted into
+    // slot 14 (BA_C_CHECK_MISMATCH) so tests see it -- per stale lane in CHECK
+    // builds (their stale-tag injection expects exactly one), once per wave
+    // otherwise
+    if constexpr (CHECK) {
+        mm += ok ? 0u : 1u;
+    } else {
+        if (!__all(ok) && lane == 0 && a.counters)
+            atomicAdd((unsigned long long*)(a.counters + BA_C_CHECK_MISMATCH), 1ull);
+    }
+    uint64_t cv[K - 1];
+    static_for<0, K - 1>([&](auto jj) {
+        cv[jj()] = (g1[jj()] << 32) | (uint32_t)g0[jj()];
+        if (act) {
+            store_sc1(gp[jj()], 0ull);
+            store_sc1(gp[jj()] + 1, 0ull);
+        }
+    });
+    casc_roots<N, ME>(a, in, scr, lane, w, lq, cv);
+}
+
 // Step q for sigma with its children cv already loaded: relay L_q[sigma.r],
 // majority, then store + arrive (q > 0) or roots + epilogue (q = 0).
 template <int N, int ME, int q, bool CHECK>
@@ -474,6 +638,7 @@ __device__ __forceinline__ void casc_finish(const CascArgs& a, const uint64_t* i
     uint32_t path[q > 0 ? q : 1], srt[q > 0 ? q : 1];
     if constexpr (q > 0) unrank_path<L, q - 1>(s, path, srt);
     const uint64_t lq = relay_slots<N, q, K, 64>(a, in, scr, lane, true, s, s * (uint32_t)K, path, gw);
+    CASC_MSTAMP(q == 0 ? 9 : 5);
     Csa<planes_c(K)> cnt;
     cnt.template add<0>(lq);
     static_for<0, K - 1>([&](auto jj) { cnt.template add<jj() + 1>(cv[jj()]); });
@@ -484,7 +649,9 @@ __device__ __forceinline__ void casc_finish(const CascArgs& a, const uint64_t* i
             return;
         }
         if (act) casc_put<N, ME, q, CHECK>(a, w, s * (uint32_t)K + r, rq);
-        drain_stores();
+        CASC_MSTAMP(6);
+        if constexpr (q != 1) drain_stores();  // R_1: granules, no drain before the arrival
+        CASC_MSTAMP(7);
         // arrive at sigma's parent (level q-2), or at the word's root counter
         constexpr uint32_t up_fan = (uint32_t)(L - (q - 1));  // children of a level q-2 slot
         const uint32_t ps = s / up_fan;
@@ -493,36 +660,13 @@ __device__ __forceinline__ void casc_finish(const CascArgs& a, const uint64_t* i
             c = a.cnt + (uint64_t)(a.cnt_off[q - 2] + w * C::sz(q - 2) + ps) * kCascCounterStride;
         else
             c = a.cnt + (uint64_t)(a.cnt_off[C::Q] + w) * kCascCounterStride;
-        if (arrive_last(c, up_fan, lane)) {
+        const bool last_ = arrive_last(c, up_fan, lane);
+        CASC_MSTAMP(8);
+        if (last_) {
             casc_step<N, ME, q - 1, CHECK>(a, in, scr, lane, w, ps, gw, tc, mm);
         }
     } else {
-        constexpr int NIN = C::NIN;
-        const uint64_t att = cnt.template ge<K, K / 2 + 1>();
-        const uint64_t tie = (K % 2 == 0) ? (cnt.template ge<K, K / 2>() & ~att) : 0ull;
-        // the epilogue overwrites bytes of its input planes: a private copy
-        if (lane < (uint32_t)NIN) scr[lane] = in[lane];
-        if (act) {
-            scr[NIN + r] = att;
-            scr[NIN + L + r] = tie;
-        }
-        __builtin_amdgcn_wave_barrier();
-        TrialCounts tw;
-        wave_epilogue<N, 1, (uint32_t)ME, 0>(scr, scr + NIN, lane, w, a.ntrials, a.decisions,
-                                            a.outcome, tw);
-        __builtin_amdgcn_wave_barrier();
-        // the word's counts, straight into the sink: every word's root step runs
-        // exactly once per launch, so the word is the sink's unit and no block
-        // barrier is needed to combine waves (a wave exits as soon as it is done)
-        uint64_t mine = 0;
-#pragma unroll
-        for (int c = 0; c < C_NUM; ++c) {
-            uint32_t x = tw.v[c];
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-            if (lane == (uint32_t)c) mine = x;
-        }
-        if (a.counters) sink_counters(lane, mine, w, a.W, a.counters, a.sk);
+        casc_roots<N, ME>(a, in, scr, lane, w, lq, cv);
         (void)tc;
     }
 }
@@ -532,9 +676,15 @@ template <int N, int ME, int q, bool CHECK, bool VIN>
 __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in, uint64_t* scr,
                                           uint32_t lane, uint32_t w, uint32_t s, uint64_t gw,
                                           TrialCounts& tc, uint32_t& mm) {
-    uint64_t cv[N - 1 - q - 1];
-    casc_kids<N, ME, q, CHECK, VIN>(a, lane, w, s, cv, mm);
-    casc_finish<N, ME, q, CHECK>(a, in, scr, lane, w, s, gw, cv, tc, mm);
+    if constexpr (q == 0 && !VIN) {  // the word's roots from the R_1 granules
+        (void)s;
+        (void)tc;
+        casc_root_step<N, ME, CHECK>(a, in, scr, lane, w, gw, mm);
+    } else {
+        uint64_t cv[N - 1 - q - 1];
+        casc_kids<N, ME, q, CHECK, VIN>(a, lane, w, s, cv, mm);
+        casc_finish<N, ME, q, CHECK>(a, in, scr, lane, w, s, gw, cv, tc, mm);
+    }
 }
 
 // One block = 4 * GPW consecutive units (their words: <= nw_max, sliced into
@@ -577,6 +727,11 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
     const uint32_t x = LAT ? y >> 1 : y, hh = LAT ? (y & 1u) : 0u;  // slot, half (LAT)
     const uint32_t u = u0 + wv * GPW + g;
     const bool act = g < (uint32_t)GPW && u < a.units;
+#ifdef BA_CASC_STAMPS
+    unsigned long long st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const unsigned long long rt_in = __builtin_amdgcn_s_memrealtime();
+    CASC_STAMP(0);
+#endif
     const uint32_t uu = act ? u : u0;
     const uint32_t w = uu / RR, rho = a.rho0 + (uu - w * RR);
     const uint64_t gw = gw0 + w;
@@ -612,6 +767,7 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
         }
         relay_draw<N, Q + 1, G, GL>(a, rp, xch, y, true, gw);
     }
+    CASC_STAMP(1);
     // 2. inputs
     if (staged) {
         if (wv < nw) stage_slice<N>(planes + wv * NIN, lane, pfm, poc, pv);
@@ -623,7 +779,9 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
             wave_inputs<N, 1, 0>(planes + k * NIN, lane, wfirst + k, a.seed, a.gs, a.first_trial,
                                  a.ntrials, a.faulty, a.order);
     }
+    CASC_STAMP(2);
     __syncthreads();
+    CASC_STAMP(3);
     // 3. the units (the leaf work sits in a divergent branch: as straight-line
     //    code for every lane the compiler's schedule needed 256 VGPRs and spilled)
     const uint64_t* in = planes + (w - wfirst) * NIN;
@@ -632,6 +790,7 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
         unrank_path<L, Q + 1>(sr, path, srt);
         const uint64_t par = relay_apply<N, Q + 1, G>(rp, in, xch, x, rho * (uint32_t)G, path);
         __builtin_amdgcn_wave_barrier();  // xch becomes the transpose below
+        CASC_STAMP(4);
         const uint64_t fs = in[path[Q + 1] + 1];  // level me-1 relayer: the slot's last lieutenant
         const uint64_t oddmask = 0ull - (uint64_t)((sr * (uint32_t)S) & 1u);
         uint64_t diag[S], Fm[S], Rm[S];
@@ -654,6 +813,7 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
         } else {
             leaf_block<S>(ME, a.seed, gw, sr, diag, Fm, Rm);
         }
+        CASC_STAMP(5);
         if (hh == 0) {
             uint64_t* t = tr + (gg * G) * GP + x;
             t[x * GP] = par;
@@ -669,8 +829,24 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
                                        CHECK && a.inject && u == 0 && x == 0);
     }
     __builtin_amdgcn_wave_barrier();
+#ifdef BA_CASC_STAMPS
+    CASC_STAMP(6);
+    drain_stores();
+    CASC_STAMP(7);
+    {
+        const uint32_t wid = blockIdx.x * kCascWaves + wv;
+        if (lane == 0 && wid < kStampWaves) {
+            for (int i = 0; i < 8; ++i) ba_lab_casc_stamps[wid][i] = st_[i];
+            ba_lab_casc_stamps[wid][8] = rt_in;
+            ba_lab_casc_stamps[wid][9] = __builtin_amdgcn_s_memrealtime();
+            ba_lab_casc_stamps[wid][10] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11)) |
+                ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (31 << 11)) << 32);
+            ba_lab_casc_stamps[wid][11] = (unsigned long long)nw | ((unsigned long long)(act ? 1 : 0) << 32);
+        }
+    }
+#endif
     if constexpr ((DIAG & 2) == 0) {
-        drain_stores();
+        if constexpr (ME - 2 != 1) drain_stores();  // R_1 (me = 3): granules, no drain
         // 4. arrivals: one lane per unit at the counter of rho's parent (level
         //    Q-1) or, at Q = 0, of the word
         bool last = false;
@@ -795,6 +971,10 @@ __global__ __launch_bounds__(256) void k_cascade_mtop(CascArgs a) {
     const uint32_t sg = act ? sg0 : s0 * (uint32_t)NG;
     TrialCounts tc;
     uint32_t mm = 0;
+    if (wv == 0) {
+        CASC_MSTAMP(14);
+        CASC_MSTAMP(0);
+    }
     // children first; the inputs (wave 0) and the relay draws overlap them
     uint64_t cv[K - 1];
     casc_kids<N, ME, Q, CHECK, false>(a, act ? r : (uint32_t)K, w, sg, cv, mm);
@@ -802,7 +982,9 @@ __global__ __launch_bounds__(256) void k_cascade_mtop(CascArgs a) {
     uint64_t* xg = xch + (wv * (uint32_t)GW + (act ? g : 0u)) * (uint32_t)M::XW;
     relay_draw<N, Q, K, K>(a, rp, xg, r, act, gw);
     if (wv == 0) wave_inputs<N, 1, 0>(planes, lane, w, a.seed, a.gs, a.first_trial, a.ntrials, a.faulty, a.order);
+    if (wv == 0) CASC_MSTAMP(1);
     __syncthreads();
+    if (wv == 0) CASC_MSTAMP(2);
     if (act) {
         uint32_t path[Q], srt[Q];
         unrank_path<L, Q - 1>(sg, path, srt);
@@ -814,8 +996,10 @@ __global__ __launch_bounds__(256) void k_cascade_mtop(CascArgs a) {
         if (a.h == (uint32_t)Q) a.votes[((uint64_t)(sg - a.ub) * K + r) * a.W + w] = rq;  // range: votes
         else rv[j * (uint32_t)K + r] = rq;
     }
+    if (wv == 0) CASC_MSTAMP(3);
     if (a.h == (uint32_t)Q) return;  // block-uniform: the range's fan-in ends at these votes
     __syncthreads();
+    if (wv == 0) CASC_MSTAMP(4);
     if (wv == 0) {
         // step Q-1 for s0: receiver r1 = lane < NG, children R_Q[s0.j1.r1], j1 != r1
         const uint32_t r1 = lane < (uint32_t)NG ? lane : 0u;
@@ -825,6 +1009,7 @@ __global__ __launch_bounds__(256) void k_cascade_mtop(CascArgs a) {
             cv1[jj()] = rv[j1 * (uint32_t)K + r1 - (r1 > j1 ? 1u : 0u)];
         });
         casc_finish<N, ME, Q - 1, CHECK>(a, planes, scr, lane, w, s0, gw, cv1, tc, mm);
+        CASC_MSTAMP(15);
     }
     if constexpr (CHECK) {
         uint32_t t = mm;
@@ -954,15 +1139,7 @@ __global__ __launch_bounds__(kWtopThreads) void k_cascade_wtop(CascArgs a) {
     if (wv == 0) {
         TrialCounts tw;
         wave_epilogue<N, 1, (uint32_t)ME, 0>(planes, au, lane, w, a.ntrials, a.decisions, a.outcome, tw);
-        uint64_t mine = 0;
-#pragma unroll
-        for (int c = 0; c < C_NUM; ++c) {
-            uint32_t x = tw.v[c];
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-            if (lane == (uint32_t)c) mine = x;
-        }
-        if (a.counters) sink_counters(lane, mine, w, a.W, a.counters, a.sk);
+        if (a.counters) sink_counters(lane, word_counts_to_lanes(tw, lane), w, a.W, a.counters, a.sk);
     }
 }
 
@@ -1267,6 +1444,24 @@ bool cascade_range_two_supported(const Geometry& g, uint32_t h) {
 #undef BA_CASC_OK
     return shape && cascade_range_supported(g, h) && g.me >= 4 && h + 4 >= g.me && h + 3 <= g.me;
 }
+
+#ifdef BA_CASC_STAMPS
+extern "C" int ba_lab_casc_stamps_read(void* dst, size_t bytes) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(ba_lab_casc_stamps), bytes, 0, hipMemcpyDeviceToHost) ==
+                   hipSuccess ? 0 : -3;
+}
+extern "C" int ba_lab_stamps_clear() {
+    static unsigned long long zero[kStampWaves][16];
+    return hipMemcpyToSymbol(HIP_SYMBOL(ba_lab_mtop_stamps), zero, sizeof zero) == hipSuccess &&
+                   hipMemcpyToSymbol(HIP_SYMBOL(ba_lab_casc_stamps), zero,
+                                     sizeof(unsigned long long) * kStampWaves * kStampWords) == hipSuccess
+               ? 0 : -3;
+}
+extern "C" int ba_lab_mtop_stamps_read(void* dst, size_t bytes) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(ba_lab_mtop_stamps), bytes, 0, hipMemcpyDeviceToHost) ==
+                   hipSuccess ? 0 : -3;
+}
+#endif
 
 bool cascade_check_supported(const Geometry& g) {
 #define BA_CASC_OK(nn, mm) if (g.n == nn && g.me == mm) return true;

@@ -627,6 +627,16 @@ constexpr size_t kSinkTaskCounterBytes = 64;  // after the replicas, a line of i
 __device__ __forceinline__ void sink_counters(uint32_t lane, uint64_t v, uint32_t unit,
                                               uint32_t nunits, uint64_t* __restrict__ out,
                                               const Sink& sk) {
+    // at most one unit per replica (small launches: a handful of words or
+    // blocks): no replica to combine in, so the unit adds straight into `out`
+    // (<= 64 adds on its line, fire and forget), which spares the latency-bound
+    // tail of a one-instance call a returning atomic and an exchange
+    if (nunits <= kSinkReplicas) {
+        if (lane < C_NUM && v)
+            (void)__hip_atomic_fetch_add((unsigned long long*)out + lane, (unsigned long long)v,
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     const uint32_t r = unit % kSinkReplicas;
     const uint32_t members = (nunits - r + kSinkReplicas - 1) / kSinkReplicas;
     if (lane < C_NUM) {

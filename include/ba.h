@@ -402,6 +402,15 @@ int ba_mt_draw_coins(ba_mt* mt, uint32_t count, uint32_t* packed, uint32_t words
 int ba_mt_table(uint32_t n, uint32_t m, uint64_t batch, const uint64_t* seeds,
                 const uint32_t* faulty_mask, const uint32_t* poll_commander, uint32_t stride,
                 uint32_t* table, uint32_t* next_word, int threads);
+/* The same table on the device (device buffers, asynchronous on `stream`, in
+ * the ctx's call order): one thread per trial seeds CPython's MT19937 and draws
+ * the round's coins; the rows equal ba_mt_table's.  Feeds ba_run_trials_device
+ * in BA_LIE_TABLE mode without a host round trip (tools/run_configs.py config 1).
+ * Uses 2,496 B of the ctx's scratch per trial of a chunk. */
+int ba_mt_table_device(struct ba_ctx* ctx, uint32_t n, uint32_t m, uint64_t batch,
+                       const uint64_t* d_seeds, const uint32_t* d_faulty_mask,
+                       const uint32_t* d_poll_commander, uint32_t stride, uint32_t* d_table,
+                       uint32_t* d_next_word, void* stream);
 
 /* Tree geometry helpers (host only, no device needed). */
 uint64_t ba_tree_slots(uint32_t n, uint32_t m);             /* sum_k |L_k|       */

@@ -166,7 +166,8 @@ def test_cascade_scratch_budget_counts_counters(monkeypatch, n, m, budget_words)
 
     def pad(k):
         g = (Lh - k + 1) * (Lh - k)
-        return ((g + 15) // 16) * 16 * (S[k - 2] if k >= 2 else 1)
+        # R_1 (the roots' hand-off) is stored as granules: two words per value
+        return ((g + 15) // 16) * 16 * (S[k - 2] if k >= 2 else 2)
     per_word = 8 * sum(pad(k) for k in range(1, me - 1)) + 128 * (1 + sum(S[k] for k in range(me - 3)))
     budget = per_word * budget_words + per_word // 2
     monkeypatch.setenv("BA_SCRATCH_BYTES", str(budget))

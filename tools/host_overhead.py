@@ -10,6 +10,10 @@ of that gap on the bench workload (n=10, m=3, 1M trials, staged inputs), with
   steps_K_sync the same, close = a plain synchronize
   enqueue      host time to enqueue K steps (no wait)
 Each line: wall us, GPU-event us, and their difference.
+
+--sched spin|yield|blocking|auto sets the HIP runtime's wait mode
+(hipSetDeviceFlags: hipDeviceScheduleSpin / Yield / BlockingSync / Auto) before
+the process's first device call, for an A/B of the close (`default`: untouched).
 """
 from __future__ import annotations
 
@@ -33,7 +37,14 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--streams", type=int, default=2)
+    ap.add_argument("--sched", default="default", choices=["default", "auto", "spin", "yield", "blocking"])
     a = ap.parse_args()
+    if a.sched != "default":
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD | os.RTLD_GLOBAL) if hasattr(os, "RTLD_NOLOAD") else None
+        flags = {"auto": 0, "spin": 1, "yield": 2, "blocking": 4}[a.sched]
+        rc = hip.hipSetDeviceFlags(flags)
+        print(json.dumps({"sched": a.sched, "hipSetDeviceFlags_rc": rc}), flush=True)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     n, m, B, NS, K = 10, 3, 1 << 20, a.streams, a.steps
@@ -104,7 +115,7 @@ def main():
         rs = [region(ns, poll) for _ in range(a.reps)]
         med = {k: round(statistics.median(r[k] for r in rs), 1) for k in rs[0]}
         mn = {k: round(min(r[k] for r in rs), 1) for k in rs[0]}
-        print(json.dumps({"variant": name, "streams": NS, "median_us": med, "min_us": mn,
+        print(json.dumps({"variant": name, "sched": a.sched, "streams": NS, "median_us": med, "min_us": mn,
                           "gap_median_us": round(med["wall"] - med["gpu"], 1)}), flush=True)
     for e in engines:
         e.close()

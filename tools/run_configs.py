@@ -8,10 +8,11 @@ ba_run_instance_split_multi; ba_amd.dist does the rendezvous).
   1  ba.py-exact mode at batch scale: OM(1) at n=4 and n=10, 1M trials, each
      trial its own ba.py round -- random.seed(seed_t), then the round's coins in
      ba.py's draw order (ba.py:45, 269) -- with random faulty sets, stale-primary
-     polls (ba.py:171) and orders.  ba_mt_table (C++, every host thread) builds the
-     coin table; k_table (ba_run_trials_device, BA_LIE_TABLE) resolves the trials
-     from it on the device.  The kernel's rate and the table's generation time are
-     reported separately (one GPU, rank 0 only).
+     polls (ba.py:171) and orders.  The coin table is built by ba_mt_table (C++,
+     every host thread) and by ba_mt_table_device (one GPU thread per trial; the
+     two tables must be equal); k_table (ba_run_trials_device, BA_LIE_TABLE)
+     resolves the trials from it.  The kernel's rate, each table's generation time
+     and both end-to-end rates are reported (one GPU, rank 0 only).
 
   3  n=13, m=4, 64M trials, trial-DP across ranks (counters all-reduced)
   4  n=10, m=3 faulty-count sweep f = 0..n/3+1, exactly f faulty, 1M trials each:
@@ -138,6 +139,41 @@ def main():
             ms = e0.elapsed_time(e1) / reps
             if any(v != first[c] * reps for c, v in counters(cnt).items()):
                 raise SystemExit("config 1: repeated calls disagree")
+            # the same table generated on the device (ba_mt_table_device: CPython's
+            # MT19937 seeded per trial, one thread each), timed with HIP events;
+            # its rows must equal the host table's
+            d_seeds = torch.from_numpy(seeds.view(np.int64)).to(dev)
+            d_tab2 = torch.empty_like(d_tab)
+
+            def gen_dev():
+                eng.mt_table_device(n, 1, T, d_seeds.data_ptr(), d_f.data_ptr(), tab.shape[1],
+                                    d_tab2.data_ptr(), d_poll=d_p.data_ptr(), stream=st.cuda_stream)
+            gen_dev()
+            torch.cuda.synchronize(dev)
+            if not torch.equal(d_tab2, d_tab):
+                raise SystemExit("config 1: device coin table differs from the host table")
+            e0.record(st)
+            for _ in range(5):
+                gen_dev()
+            e1.record(st)
+            torch.cuda.synchronize(dev)
+            ms_gen = e0.elapsed_time(e1) / 5
+
+            def both():  # table generation + the trials, back to back on the stream
+                gen_dev()
+                eng.run_device(p, T, d_faulty=d_f.data_ptr(), d_order=d_o.data_ptr(),
+                               d_table=d_tab2.data_ptr(), d_poll=d_p.data_ptr(),
+                               d_decisions=dec.data_ptr(), d_outcome=outc.data_ptr(),
+                               d_counters=cnt.data_ptr(), stream=st.cuda_stream)
+            cnt.zero_()
+            e0.record(st)
+            for _ in range(5):
+                both()
+            e1.record(st)
+            torch.cuda.synchronize(dev)
+            ms_both = e0.elapsed_time(e1) / 5
+            if any(v != first[c] * 5 for c, v in counters(cnt).items()):
+                raise SystemExit("config 1: device-table runs disagree")
             out.append({"config": 1, "workload": f"ba.py OM(1) bit-exact, n={n}, {T} trials, one "
                         "MT19937 seed per trial (random.seed + the round's coins in ba.py's draw "
                         "order), random faulty sets / stale-primary polls / orders",
@@ -149,8 +185,15 @@ def main():
                         "table_threads": threads or os.cpu_count(),
                         "table_bytes": int(tab.nbytes), "h2d_s": t_h2d,
                         "end_to_end_trials_per_s": T / (t_tab + t_h2d + ms * 1e-3),
+                        "end_to_end_note": "host table (ba_mt_table) + H2D + kernel",
+                        "device_table_ms": ms_gen,
+                        "device_table_trials_per_s": T / (ms_gen * 1e-3),
+                        "device_end_to_end_trials_per_s": T / (ms_both * 1e-3),
+                        "device_end_to_end_note": "ba_mt_table_device + k_table back to back on "
+                                                  "one stream (seeds, faulty sets, polls, orders in "
+                                                  "HBM; HIP events), table equal to the host's",
                         "n_gpus": 1, "counters": first})
-            del d_tab, d_f, d_p, d_o, dec, outc
+            del d_tab, d_tab2, d_seeds, d_f, d_p, d_o, dec, outc
 
     if 3 in which:
         n, m, T = 13, 4, a.trials3
