@@ -199,7 +199,7 @@ __device__ __forceinline__ void philox10_n_vk(P4 (&c)[G], const KeysV& kv) {
             c[g] = n;
         }
     });
-    if constexpr (G >= 2 && G <= 4) {
+    if constexpr (G >= 2 && G <= 5) {
         uint32_t rk0[8], rk1[8], x[G], y[G], z[G], w[G];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -238,7 +238,7 @@ __host__ __device__ __forceinline__ void philox10_n(P4 (&c)[G], uint32_t k0, uin
 #if defined(__HIP_DEVICE_COMPILE__)
     // round keys as VGPR operands (KeysV, hoisted by the compiler): Philox calls
     // 8.4e11 -> 9.6e11 per second at 2 waves/SIMD (tools/philox_bench)
-    if constexpr (G >= 2 && G <= 4) {
+    if constexpr (G >= 2 && G <= 5) {
         philox10_n_vk<G>(c, KeysV(k0, k1));
         return;
     }

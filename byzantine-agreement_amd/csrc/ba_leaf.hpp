@@ -25,11 +25,14 @@ __device__ __forceinline__ void static_for(F&& f) {
 // counters see a compile-time input schedule (Csa, ba_device.hpp).
 // The S(S-1)/2 Philox calls run in interleaved groups of PG (philox10_n);
 // each group's 2*PG lie words feed the counters before the next group starts.
-#ifdef BA_LEAF_PG  // lab builds: force the group size where it divides the pair count
-constexpr int leaf_philox_group(int npair) { return npair % BA_LEAF_PG == 0 ? BA_LEAF_PG : (npair % 3 == 0 ? 3 : (npair % 4 == 0 ? 4 : (npair % 2 == 0 ? 2 : 3))); }
-#else
-constexpr int leaf_philox_group(int npair) { return npair % 3 == 0 ? 3 : (npair % 4 == 0 ? 4 : (npair % 2 == 0 ? 2 : 3)); }
-#endif
+// The S = 11 leaf (config 5, n=16 m=5: 55 pairs) in groups of 5: 11 full groups
+// where groups of 3 left a lone call at the end; one lease, A B A B
+// (profiles/r05i_c5_leaf_groups_ab.log): 1024-instance calls 59.4-60.4 vs
+// 60.7-61.1 us on one stream, 48.7-49.4 vs 49.9-50.3 us with two in flight
+// (groups of 6: 61.9-62.5); one instance 16.8-16.9 vs 16.5 us.
+constexpr int leaf_philox_group(int npair) {
+    return npair == 55 ? 5 : (npair % 3 == 0 ? 3 : (npair % 4 == 0 ? 4 : (npair % 2 == 0 ? 2 : 3)));
+}
 
 // Column-ordered schedule (S - 1 even: a slot pair never straddles two rows).
 // Step t takes pair q(t) = a (S-1)/2 + cp with cp = t / S, a = t % S: the pairs

@@ -112,8 +112,8 @@ def run_asm(lines, outs, ins, env):
 
 
 # the shipped variant (product header) and the --lab ones
-@pytest.mark.parametrize("name", ["philox_r29_asm_vkm", "philox_r29_asm", "philox_r29_asm_vk"])
-@pytest.mark.parametrize("G", [2, 3, 4])
+@pytest.mark.parametrize("name,G", [("philox_r29_asm_vkm", g) for g in (2, 3, 4, 5)] +
+                         [(nm, g) for nm in ("philox_r29_asm", "philox_r29_asm_vk") for g in (2, 3, 4)])
 def test_generated_rounds_match_philox(G, name):
     lines, outs, ins = parse(G, name)
     rng = random.Random(1234 + G)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Generate csrc/ba_philox_asm.hpp: Philox4x32-10 rounds 2..9 of G interleaved
-calls as ONE inline-asm statement (G = 2, 3, 4).
+calls as ONE inline-asm statement (G = 2..5; the SGPR-key lab variants G = 2, 3, 4).
 
 Why: the products of rounds 2..9 are pinned to v_mad_u64_u32 with inline asm
 (ba_device.hpp, philox_mul2_n).  The compiler's hazard recognizer cannot see
@@ -150,7 +150,10 @@ def gen(G: int, kc: str = "s", mc: str = "s") -> str:
                 clob.append(f'"v{q}"')
     for g in range(G):
         ops_out = [o.replace(f"vW{g}}}", f"v{outs_w[g]}}}").replace(f"vY{g}}}", f"v{outs_y[g]}}}") for o in ops_out]
-    body = "\n".join(f'        "{l}\\n\\t"' for l in lines[:-1]) + f'\n        "{lines[-1]}"'
+    # one source line per phase of a round (its G products or its G xor3s):
+    # the asm text is the same instruction string, a quarter as many lines
+    text = [l + ("\\n\\t" if k + 1 < len(lines) else "") for k, l in enumerate(lines)]
+    body = "\n".join('        "' + "".join(text[k:k + G]) + '"' for k in range(0, len(text), G))
     fname = "philox_r29_asm" if kc == "s" else ("philox_r29_asm_vk" if mc == "s" else "philox_r29_asm_vkm")
     mparams = "" if mc == "s" else ",\n                                                 uint32_t m0, uint32_t m1"
     return f"""template <>
@@ -167,6 +170,9 @@ __device__ __forceinline__ void {fname}<{G}>(uint32_t (&x)[{G}], uint32_t (&y)[{
         : {", ".join(clob)});
 }}
 """
+
+
+GS = (2, 3, 4, 5)  # call-group sizes of the shipped variant (philox10_n: G = 2..5)
 
 
 def main():
@@ -205,7 +211,7 @@ def main():
             out.append(gen(G))
         for G in (2, 3, 4):
             out.append(gen(G, "v"))
-    for G in (2, 3, 4):
+    for G in GS:
         out.append(gen(G, "v", "v"))
     out.append('#endif')
     out.append('}  // namespace ba')

@@ -2,7 +2,7 @@
 # GPU-box session: every GPU step has its own time limit; a fault, abort or
 # timeout ends the session (no retries).  Logs land in gpurun_out/.
 # usage: tools/gpu_session.sh [stage ...]
-#   tests smoke bench bench2 bench_levels bench_fused prof prof1 pmc philox configs
+#   tests smoke bench bench2 bench_levels bench_fused prof prof1 pmc philox configs sched
 #   (prof: the default bench command, two steps in flight, so each k_om3w launch
 #   spans ~2x its own time; prof1: --streams 1, the launch time the roofline uses)
 set -u
@@ -58,6 +58,10 @@ for s in $STAGES; do
          pmc_pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR || exit $?
          python3 tools/pmc_summary.py gpurun_out/pmc gpurun_out/pmc_summary.json \
            --workload "bench.py default: n=10 m=3, 1048576 trials/step" --config 10,3,1048576,auto,k_om3w > gpurun_out/pmc_summary.log 2>&1 ;;
+    sched) for m in default spin yield blocking default spin; do
+             run sched_$m 300 python -u tools/host_overhead.py --sched $m || exit $?
+             cat gpurun_out/sched_$m.log >> gpurun_out/sched_all.jsonl
+           done ;;
     configs) run configs 600 python -u tools/run_configs.py || exit $? ;;
     c5) run c5_1024 300 python -u tools/config5_prof.py --batch 1024 --split || exit $?
         run c5_1 300 python -u tools/config5_prof.py --batch 1 --reps 500 --split || exit $? ;;
