@@ -606,6 +606,7 @@ static bool use_cascade(ba_ctx* ctx, const Geometry& g) {
 }
 
 constexpr uint64_t kCascTwoWords = 1;
+constexpr uint64_t kCascCoWords = 2;
 
 // BA_CASC_CHECK (tests only, read per call): 1 = the cascade's check build
 // (epoch tags beside every hand-off word, mismatches counted into
@@ -636,11 +637,23 @@ static int run_cascade(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge, CascJob job 
         const char* e = getenv("BA_CASC_TWO");
         job.two = e ? atoi(e) != 0 : (a.batch + 63) / 64 >= kCascTwoWords;
     }
+    // The whole tree as ONE launch of units + co-resident fan-in blocks (no
+    // units -> fan-in kernel boundary; ba_cascade.hip casc_co_top) up to
+    // kCascCoWords 64-trial words.  BA_CASC_CO=0/1 (read per call) forces it.
+    if (job.two && job.h == 0) {
+        const char* e = getenv("BA_CASC_CO");
+        job.co = e ? atoi(e) != 0 : (a.batch + 63) / 64 <= kCascCoWords;
+    }
     // per trial word: R_1 .. R_{me-2} (twice with check tags) and the fan-in
     // counters, one 128-B line each -- both count against the scratch budget
     // The split's root pass as k_cascade_wtop uses neither (the default)
     const bool uses = !job.vin || cascade_root_pass_uses_scratch();
-    const uint64_t r_bytes = uses ? cascade_scratch_words_per_word(g) * sizeof(uint64_t) *
+    if (job.co) {  // CO keeps R_{me-2} as granules (2x): only where the batch fits one chunk
+        const uint64_t co_bytes = cascade_scratch_words_per_word(g, true) * sizeof(uint64_t) *
+                                      (job.check ? 2 : 1) + cascade_counters_per_word(g) * 128;
+        if (ctx->scratch_budget / co_bytes < (a.batch + 63) / 64) job.co = false;
+    }
+    const uint64_t r_bytes = uses ? cascade_scratch_words_per_word(g, job.co) * sizeof(uint64_t) *
                                         (job.check ? 2 : 1) : 0;
     const uint64_t c_bytes = uses ? cascade_counters_per_word(g) * 128 : 0;
     const uint64_t words = (a.batch + 63) / 64;

@@ -72,9 +72,14 @@ __device__ unsigned long long ba_lab_mtop_stamps[kStampWaves][16];
             ba_lab_mtop_stamps[blockIdx.x][i] = (i) >= 14 ? __builtin_amdgcn_s_memrealtime() \
                                                           : __builtin_amdgcn_s_memtime(); \
     } while (0)
+#define CASC_MVAL(i, v)                                                                  \
+    do {                                                                                 \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < kStampWaves) ba_lab_mtop_stamps[blockIdx.x][i] = (v); \
+    } while (0)
 #else
 #define CASC_STAMP(i) ((void)0)
 #define CASC_MSTAMP(i) ((void)0)
+#define CASC_MVAL(i, v) ((void)0)
 #endif
 
 constexpr int kCascMaxLevels = 8;
@@ -108,6 +113,7 @@ struct CascArgs {
     uint32_t ub;          // range mode: first h-hop subtree of the range
     uint32_t ue;          // range mode: one past the last
     uint32_t s0b, s0n;    // k_cascade_mtop: its level-(me-5) slots per word, [s0b, s0b + s0n)
+    uint32_t nub;         // CO launches: blocks [0, nub) run units, the rest the fan-in
     uint64_t* votes;      // range mode: [(u - ub)(L - h) + c][W]
     const uint64_t* vin;  // root mode: every unit's votes, [level-h slot][W]
     uint64_t* decisions;  // chunk-relative
@@ -131,8 +137,9 @@ constexpr uint32_t casc_ngrp(int L, int k) { return k >= 2 ? casc_sz(L, k - 2) :
 // R_1 (the hand-off into the roots) is stored as granules: two 8-byte {value
 // half, epoch tag} words per value (casc_put / casc_kids), so its level takes
 // twice the words
-constexpr uint64_t casc_level_words(int L, int k) {
-    return (uint64_t)casc_ngrp(L, k) * casc_pad(L, k) * (k == 1 ? 2u : 1u);
+// (and in CO launches so is R_{me-2}, the units' hand-off: `gran`)
+constexpr uint64_t casc_level_words(int L, int k, bool gran = false) {
+    return (uint64_t)casc_ngrp(L, k) * casc_pad(L, k) * (k == 1 || gran ? 2u : 1u);
 }
 
 template <int N, int ME>
@@ -453,6 +460,12 @@ __device__ __forceinline__ uint64_t relay_slots(const CascArgs& a, const uint64_
 constexpr uint32_t kGranuleSpinCap = 1u << 16;  // s_sleep 1 polls before giving up (~ms)
 __device__ __forceinline__ uint32_t casc_gtag(uint64_t epoch) { return ((uint32_t)epoch << 1) | 1u; }
 
+// A relay value computed ahead of its step (CO fan-in blocks), or none.
+struct Pre {
+    bool on = false;
+    uint64_t v = 0;
+};
+
 // R store of one hand-off word (+ its tag in CHECK builds): write-through;
 // level 1 as two granules
 template <int N, int ME, int k, bool CHECK>
@@ -506,7 +519,7 @@ __device__ __forceinline__ void casc_kids(const CascArgs& a, uint32_t lane, uint
 template <int N, int ME, int q, bool CHECK, bool VIN = false>
 __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in, uint64_t* scr,
                                           uint32_t lane, uint32_t w, uint32_t s, uint64_t gw,
-                                          TrialCounts& tc, uint32_t& mm);
+                                          TrialCounts& tc, uint32_t& mm, Pre l0 = Pre{});
 
 // The word's per-lane run counts of a one-word epilogue (wave_epilogue, W = 1:
 // only lanes 0..7, one byte of trials each, hold counts) to lane c = counter c:
@@ -569,7 +582,8 @@ __device__ __forceinline__ void casc_roots(const CascArgs& a, const uint64_t* in
 // (each has exactly one reader: receiver r of its slot).
 template <int N, int ME, bool CHECK>
 __device__ __forceinline__ void casc_root_step(const CascArgs& a, const uint64_t* in, uint64_t* scr,
-                                               uint32_t lane, uint32_t w, uint64_t gw, uint32_t& mm) {
+                                               uint32_t lane, uint32_t w, uint64_t gw, uint32_t& mm,
+                                               Pre l0 = Pre{}) {
     using C = Casc<N, ME>;
     constexpr int L = C::L, K = L;
     const bool act = lane < (uint32_t)K;
@@ -584,7 +598,8 @@ __device__ __forceinline__ void casc_root_step(const CascArgs& a, const uint64_t
         g1[jj()] = act ? load_sc1(gp[jj()] + 1) : 0ull;
     });
     uint32_t path[1];
-    const uint64_t lq = relay_slots<N, 0, K, 64>(a, in, scr, lane, true, 0u, 0u, path, gw);
+    // l0: L_0 relayed ahead (a CO fan-in block does it while it waits)
+    const uint64_t lq = l0.on ? l0.v : relay_slots<N, 0, K, 64>(a, in, scr, lane, true, 0u, 0u, path, gw);
     CASC_MSTAMP(9);
     auto fresh = [&]() {
         bool ok = true;
@@ -625,11 +640,13 @@ __device__ __forceinline__ void casc_root_step(const CascArgs& a, const uint64_t
 
 // Step q for sigma with its children cv already loaded: relay L_q[sigma.r],
 // majority, then store + arrive (q > 0) or roots + epilogue (q = 0).
+// lqp / l0 (CO fan-in blocks): L_q[sigma.lane] / L_0[lane] relayed ahead, while
+// the block waited for the units.
 template <int N, int ME, int q, bool CHECK>
 __device__ __forceinline__ void casc_finish(const CascArgs& a, const uint64_t* in, uint64_t* scr,
                                             uint32_t lane, uint32_t w, uint32_t s, uint64_t gw,
                                             const uint64_t (&cv)[N - 1 - q - 1], TrialCounts& tc,
-                                            uint32_t& mm) {
+                                            uint32_t& mm, Pre lqp = Pre{}, Pre l0 = Pre{}) {
     using C = Casc<N, ME>;
     constexpr int L = C::L, K = L - q;
     const bool act = lane < (uint32_t)K;
@@ -637,7 +654,8 @@ __device__ __forceinline__ void casc_finish(const CascArgs& a, const uint64_t* i
     // L_q[sigma.r], sigma's path unranked (no tables)
     uint32_t path[q > 0 ? q : 1], srt[q > 0 ? q : 1];
     if constexpr (q > 0) unrank_path<L, q - 1>(s, path, srt);
-    const uint64_t lq = relay_slots<N, q, K, 64>(a, in, scr, lane, true, s, s * (uint32_t)K, path, gw);
+    const uint64_t lq = lqp.on ? lqp.v
+                               : relay_slots<N, q, K, 64>(a, in, scr, lane, true, s, s * (uint32_t)K, path, gw);
     CASC_MSTAMP(q == 0 ? 9 : 5);
     Csa<planes_c(K)> cnt;
     cnt.template add<0>(lq);
@@ -655,19 +673,27 @@ __device__ __forceinline__ void casc_finish(const CascArgs& a, const uint64_t* i
         // arrive at sigma's parent (level q-2), or at the word's root counter
         constexpr uint32_t up_fan = (uint32_t)(L - (q - 1));  // children of a level q-2 slot
         const uint32_t ps = s / up_fan;
-        uint32_t* c;
-        if constexpr (q - 1 >= 1)
-            c = a.cnt + (uint64_t)(a.cnt_off[q - 2] + w * C::sz(q - 2) + ps) * kCascCounterStride;
-        else
-            c = a.cnt + (uint64_t)(a.cnt_off[C::Q] + w) * kCascCounterStride;
-        const bool last_ = arrive_last(c, up_fan, lane);
+        bool last_;
+        if (q == 1 && a.nub != 0) {
+            // a CO launch: no arrival -- the word's s0 = 0 block takes the roots,
+            // polling the other blocks' R_1 granules (casc_root_step) as they land
+            last_ = s == 0;
+        } else {
+            uint32_t* c;
+            if constexpr (q - 1 >= 1)
+                c = a.cnt + (uint64_t)(a.cnt_off[q - 2] + w * C::sz(q - 2) + ps) * kCascCounterStride;
+            else
+                c = a.cnt + (uint64_t)(a.cnt_off[C::Q] + w) * kCascCounterStride;
+            last_ = arrive_last(c, up_fan, lane);
+        }
         CASC_MSTAMP(8);
         if (last_) {
-            casc_step<N, ME, q - 1, CHECK>(a, in, scr, lane, w, ps, gw, tc, mm);
+            casc_step<N, ME, q - 1, CHECK>(a, in, scr, lane, w, ps, gw, tc, mm, q == 1 ? l0 : Pre{});
         }
     } else {
         casc_roots<N, ME>(a, in, scr, lane, w, lq, cv);
         (void)tc;
+        (void)l0;
     }
 }
 
@@ -675,15 +701,193 @@ __device__ __forceinline__ void casc_finish(const CascArgs& a, const uint64_t* i
 template <int N, int ME, int q, bool CHECK, bool VIN>
 __device__ __forceinline__ void casc_step(const CascArgs& a, const uint64_t* in, uint64_t* scr,
                                           uint32_t lane, uint32_t w, uint32_t s, uint64_t gw,
-                                          TrialCounts& tc, uint32_t& mm) {
+                                          TrialCounts& tc, uint32_t& mm, Pre l0) {
     if constexpr (q == 0 && !VIN) {  // the word's roots from the R_1 granules
         (void)s;
         (void)tc;
-        casc_root_step<N, ME, CHECK>(a, in, scr, lane, w, gw, mm);
+        casc_root_step<N, ME, CHECK>(a, in, scr, lane, w, gw, mm, l0);
     } else {
+        (void)l0;
         uint64_t cv[N - 1 - q - 1];
         casc_kids<N, ME, q, CHECK, VIN>(a, lane, w, s, cv, mm);
         casc_finish<N, ME, q, CHECK>(a, in, scr, lane, w, s, gw, cv, tc, mm);
+    }
+}
+
+// The fan-in block's shape (k_cascade_mtop, and the fan-in blocks of a CO
+// launch): one block per (word, level-(Q-2) slot s0), step Q for its NG sigmas.
+template <int N, int ME>
+struct CascMtop {
+    using C = Casc<N, ME>;
+    static constexpr int L = C::L, Q = C::Q, K = L - Q;  // step Q: K receivers per sigma
+    static constexpr int NG = L - (Q - 1);                // sigmas per block (children of s0)
+    static constexpr int GW = 64 / K;                     // sigma groups per wave
+    static constexpr int NWV = (NG + GW - 1) / GW;        // waves per block
+    static constexpr uint32_t PB = Q >= 2 ? C::sz(Q - 2) : 1u;  // blocks per word
+    static constexpr int XW = 2 * RelayPlan<N, (Q >= 1 ? Q : 1), K>::CALLS;  // relay words per group
+    // LDS words of one fan-in block: planes, relay exchange, R_Q of the sigmas, step scratch
+    static constexpr uint32_t oXCH = (C::NIN + 1) & ~1, oRV = oXCH + NWV * GW * XW,
+                              oSCR = oRV + ((NG * K + 1) & ~1), oXQ1 = oSCR + 64,
+                              oX0 = oXQ1 + 2 * RelayPlan<N, (Q >= 1 ? Q - 1 : 0), NG>::CALLS,
+                              words = oX0 + 2 * RelayPlan<N, 0, L>::CALLS;
+};
+
+// CO launches: one launch holds the units AND the fan-in blocks (blocks
+// [nub, nub + W * PB)), so the units -> fan-in hop is no kernel boundary.  A
+// fan-in block is k_cascade_mtop's, except that it starts while the units run:
+// it draws its relays (and the later steps' Philox pairs) and slices its word's
+// inputs at once, then each wave polls its sigmas' children R_{me-2} -- granules,
+// {value half, epoch tag} in one 8-B sc1 store (MI355X_MICROARCH.md's R2 form),
+// so the units neither drain nor count -- until every lane's carry this launch's
+// tag, and zeroes them for the next launch (each granule has one reader).  The
+// poll is bounded (kCoWaitTicks of s_memrealtime; a granule still stale then is
+// counted into BA_C_CHECK_MISMATCH).  Forward progress needs no dispatch order:
+// a polling block waits only for units blocks, which wait for nothing, and the
+// polling blocks of a launch (W * PB: 15 per word at n=16, m=5) are far fewer
+// than the chip's block slots.
+constexpr uint64_t kCoWaitTicks = 20000000;  // s_memrealtime (100 MHz): 200 ms
+
+template <int N, int ME, bool CHECK>
+__device__ __forceinline__ void casc_co_top(const CascArgs& a, uint64_t* lds, uint32_t bid) {
+    using C = Casc<N, ME>;
+    using M = CascMtop<N, ME>;
+    constexpr int L = M::L, Q = M::Q, K = M::K, NG = M::NG, GW = M::GW;
+    static_assert(Q >= 1 && M::NWV <= (int)kCascWaves, "CO fan-in: me >= 4, <= 4 waves");
+    uint64_t* planes = lds + 0;
+    uint64_t* xch = lds + M::oXCH;
+    uint64_t* rv = lds + M::oRV;
+    uint64_t* scr = lds + M::oSCR;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t w = bid / M::PB, s0 = bid - w * M::PB;
+    const uint64_t gw = (a.first_trial >> 6) + w;
+    const uint32_t g = lane / (uint32_t)K, r = lane - g * (uint32_t)K;
+    const uint32_t j = wv * (uint32_t)GW + g;  // sigma = child j of s0
+    const bool act = g < (uint32_t)GW && j < (uint32_t)NG;
+    const uint32_t sg = s0 * (uint32_t)NG + (act ? j : 0u);
+    TrialCounts tc;
+    uint32_t mm = 0;
+    if (wv == 0) {
+        CASC_MSTAMP(14);
+        CASC_MSTAMP(0);
+    }
+    // 1. everything that needs no unit: step Q's relay draws, the word's inputs
+    const RelayPlan<N, Q, K> rp(sg, sg * (uint32_t)K);
+    uint64_t* xg = xch + (act ? (wv * (uint32_t)GW + g) * (uint32_t)M::XW : 0u);
+    relay_draw<N, Q, K, K>(a, rp, xg, r, act, gw);
+    if (wv == 0) wave_inputs<N, 1, 0>(planes, lane, w, a.seed, a.gs, a.first_trial, a.ntrials, a.faulty, a.order);
+    //    and the later steps' draws: L_{Q-1}[s0.*] (step Q-1) and L_0 (the
+    //    roots, should this block's arrival be the word's last), off the chain
+    //    that starts when the units are in
+    if (wv == kCascWaves - 1) {
+        relay_draw<N, Q - 1, NG, 64>(a, RelayPlan<N, Q - 1, NG>(s0, s0 * (uint32_t)NG), lds + M::oXQ1, lane,
+                                     true, gw);
+        if constexpr (Q - 1 > 0)
+            relay_draw<N, 0, L, 64>(a, RelayPlan<N, 0, L>(0u, 0u), lds + M::oX0, lane, true, gw);
+    }
+    if (wv == 0) CASC_MSTAMP(1);
+    __syncthreads();  // the planes (wave 0) and the later steps' draws (wave 3) are in LDS
+    //    every relay value the block's steps need, while the units still run:
+    //    L_Q[sigma.r] per group lane; wave 0 also L_{Q-1}[s0.lane] and L_0[lane]
+    uint64_t lqQ = 0;
+    if (act) {
+        uint32_t path[Q], srt[Q];
+        unrank_path<L, Q - 1>(sg, path, srt);
+        lqQ = relay_apply<N, Q, K>(rp, planes, xg, r, sg * (uint32_t)K, path);
+    }
+    Pre p1, p0;
+    if (wv == 0) {
+        uint32_t path1[Q > 1 ? Q - 1 : 1], srt1[Q > 1 ? Q - 1 : 1];
+        if constexpr (Q > 1) unrank_path<L, Q - 2>(s0, path1, srt1);
+        p1.on = true;
+        p1.v = relay_apply<N, Q - 1, NG>(RelayPlan<N, Q - 1, NG>(s0, s0 * (uint32_t)NG), planes, lds + M::oXQ1,
+                                         lane, s0 * (uint32_t)NG, path1);
+        if constexpr (Q > 1) {
+            uint32_t path0[1];
+            p0.on = true;
+            p0.v = relay_apply<N, 0, L>(RelayPlan<N, 0, L>(0u, 0u), planes, lds + M::oX0, lane, 0u, path0);
+        }
+    }
+    // 2. the children R_{Q+1}[sigma.jc.r], jc != r: granules, polled by each wave
+    //    until all of its lanes' carry this launch's tag (the data is its own
+    //    flag: no counter, no drain on the units' side), s_memrealtime-bounded
+    const uint32_t tag = casc_gtag(a.epoch);
+    uint64_t* gp[K - 1];
+    uint64_t g0[K - 1], g1[K - 1];
+    static_for<0, K - 1>([&](auto jj) {
+        const uint32_t jc = (uint32_t)jj() + ((uint32_t)jj() >= r ? 1u : 0u);
+        const uint32_t x = (sg * (uint32_t)K + jc) * (uint32_t)(K - 1) + r - (r > jc ? 1u : 0u);
+        gp[jj()] = a.R[Q + 1] + 2 * C::template addr<Q + 1>(w, act ? x : 0u);
+    });
+    auto load_all = [&]() {
+        static_for<0, K - 1>([&](auto jj) {
+            g0[jj()] = act ? load_sc1(gp[jj()]) : 0ull;
+            g1[jj()] = act ? load_sc1(gp[jj()] + 1) : 0ull;
+        });
+    };
+    auto fresh = [&]() {
+        bool ok = true;
+        static_for<0, K - 1>([&](auto jj) {
+            ok &= !act || ((uint32_t)(g0[jj()] >> 32) == tag && (uint32_t)(g1[jj()] >> 32) == tag);
+        });
+        return ok;
+    };
+    if (wv == 0) CASC_MSTAMP(2);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t polls = 0;
+    load_all();
+    bool ok = fresh();
+    while (!__all(ok)) {  // wave-uniform
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kCoWaitTicks) break;
+        __builtin_amdgcn_s_sleep(2);
+        load_all();
+        ok = fresh();
+        ++polls;
+    }
+    if (wv == 0) {
+        CASC_MVAL(12, __builtin_amdgcn_s_memrealtime());
+        CASC_MVAL(13, (unsigned long long)polls);
+    }
+    (void)polls;
+    if constexpr (CHECK) {
+        mm += ok ? 0u : 1u;
+    } else {
+        if (!__all(ok) && lane == 0 && a.counters)
+            atomicAdd((unsigned long long*)(a.counters + BA_C_CHECK_MISMATCH), 1ull);
+    }
+    uint64_t cv[K - 1];
+    static_for<0, K - 1>([&](auto jj) {
+        cv[jj()] = (g1[jj()] << 32) | (uint32_t)g0[jj()];
+        if (act) {
+            store_sc1(gp[jj()], 0ull);
+            store_sc1(gp[jj()] + 1, 0ull);
+        }
+    });
+    if (wv == 0) CASC_MSTAMP(3);
+    // 4. step Q for the sigmas into LDS, then step Q-1 for s0 (k_cascade_mtop)
+    if (act) {
+        Csa<planes_c(K)> cnt;
+        cnt.template add<0>(lqQ);
+        static_for<0, K - 1>([&](auto jj) { cnt.template add<jj() + 1>(cv[jj()]); });
+        rv[j * (uint32_t)K + r] = cnt.template ge<K, K / 2 + 1>();  // inner tie -> non-attack
+    }
+    __syncthreads();
+    if (wv == 0) {
+        CASC_MSTAMP(4);
+        const uint32_t r1 = lane < (uint32_t)NG ? lane : 0u;
+        uint64_t cv1[NG - 1];
+        static_for<0, NG - 1>([&](auto jj) {
+            const uint32_t j1 = (uint32_t)jj() + ((uint32_t)jj() >= r1 ? 1u : 0u);
+            cv1[jj()] = rv[j1 * (uint32_t)K + r1 - (r1 > j1 ? 1u : 0u)];
+        });
+        casc_finish<N, ME, Q - 1, CHECK>(a, planes, scr, lane, w, s0, gw, cv1, tc, mm, p1, p0);
+        CASC_MSTAMP(15);
+    }
+    if constexpr (CHECK) {
+        uint32_t t = mm;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+        if (lane == 0 && t != 0 && a.counters)
+            atomicAdd((unsigned long long*)(a.counters + BA_C_CHECK_MISMATCH), (unsigned long long)t);
     }
 }
 
@@ -710,10 +914,18 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
     constexpr int L = C::L, S = C::S, G = C::G, GP = C::GP, GPW = U::GPW, NIN = C::NIN, Q = C::Q;
     constexpr int GL = U::GL;
     static_assert(!LAT || (DIAG & 2) != 0, "latency mode: units-only launches");
+    constexpr bool CO = (DIAG & 8) != 0;  // units + co-resident fan-in blocks (casc_co_top)
+    static_assert(!CO || ((DIAG & 2) != 0 && !LAT), "CO: units-only body, normal lanes");
     constexpr int NPD = (S + 1) / 2;
     constexpr uint32_t fan = (uint32_t)(L - Q);  // children of a level Q-1 slot (or of the root)
     using RP = RelayPlan<N, Q + 1, G>;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    if constexpr (CO) {
+        if (blockIdx.x >= a.nub) {  // block-uniform
+            casc_co_top<N, ME, CHECK>(a, lds, blockIdx.x - a.nub);
+            return;
+        }
+    }
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t RR = a.rr;  // units per word
     const uint32_t u0 = blockIdx.x * kCascWaves * GPW;
@@ -825,8 +1037,16 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade(CascArgs a) {
         const uint64_t* col = tr + (gg * G + x) * GP;
         Csa<planes_c(G)> cnt;
         static_for<0, G>([&](auto b) { cnt.template add<b()>(col[b()]); });
-        casc_put<N, ME, ME - 2, CHECK>(a, w, sr, cnt.template ge<G, G / 2 + 1>(),
-                                       CHECK && a.inject && u == 0 && x == 0);
+        const uint64_t rv = cnt.template ge<G, G / 2 + 1>();
+        const bool stale = CHECK && a.inject && u == 0 && x == 0;
+        if constexpr (CO) {  // two granules: the fan-in block polls them (no drain, no arrival)
+            const uint64_t i = C::template addr<ME - 2>(w, sr);
+            const uint64_t tg = (uint64_t)casc_gtag(stale ? a.epoch - 1 : a.epoch) << 32;
+            store_sc1(a.R[ME - 2] + 2 * i, tg | (uint32_t)rv);
+            store_sc1(a.R[ME - 2] + 2 * i + 1, tg | (uint32_t)(rv >> 32));
+        } else {
+            casc_put<N, ME, ME - 2, CHECK>(a, w, sr, rv, stale);
+        }
     }
     __builtin_amdgcn_wave_barrier();
 #ifdef BA_CASC_STAMPS
@@ -939,17 +1159,6 @@ __global__ __launch_bounds__(64 * kCascWaves) void k_cascade_top(CascArgs a) {
 // Q-1 through memory (store, drain, returning add, reload); here that hop is
 // one barrier.
 // ---------------------------------------------------------------------------
-template <int N, int ME>
-struct CascMtop {
-    using C = Casc<N, ME>;
-    static constexpr int L = C::L, Q = C::Q, K = L - Q;  // step Q: K receivers per sigma
-    static constexpr int NG = L - (Q - 1);                // sigmas per block (children of s0)
-    static constexpr int GW = 64 / K;                     // sigma groups per wave
-    static constexpr int NWV = (NG + GW - 1) / GW;        // waves per block
-    static constexpr uint32_t PB = Q >= 2 ? C::sz(Q - 2) : 1u;  // blocks per word
-    static constexpr int XW = 2 * RelayPlan<N, (Q >= 1 ? Q : 1), K>::CALLS;  // relay words per group
-};
-
 template <int N, int ME, bool CHECK = false>
 __global__ __launch_bounds__(256) void k_cascade_mtop(CascArgs a) {
     using C = Casc<N, ME>;
@@ -1219,9 +1428,10 @@ uint64_t cascade_counters_per_word(const Geometry& g) {
 }
 
 // R_1 .. R_{me-2} of one word, each step's child block padded to whole lines
-uint64_t cascade_scratch_words_per_word(const Geometry& g) {
+// (co: R_{me-2} as granules, a CO launch's units -> fan-in hand-off)
+uint64_t cascade_scratch_words_per_word(const Geometry& g, bool co) {
     uint64_t s = 0;
-    for (uint32_t k = 1; k + 2 <= g.me; ++k) s += casc_level_words((int)g.L, (int)k);
+    for (uint32_t k = 1; k + 2 <= g.me; ++k) s += casc_level_words((int)g.L, (int)k, co && k + 2 == g.me);
     return s;
 }
 
@@ -1233,6 +1443,20 @@ bool cascade_range_supported(const Geometry& g, uint32_t h) {
     BA_CASC_RANGE_SHAPES(BA_CASC_OK)
 #undef BA_CASC_OK
     return shape && (h == 1 || h == 2) && h + 3 <= g.me;
+}
+
+// CO launch: the units blocks, then W * PB fan-in blocks (casc_co_top)
+template <int N, int ME, bool CHECK = false>
+static hipError_t launch_cascade_co(CascArgs& ca, hipStream_t st) {
+    using U = CascU<N, ME, false>;
+    using M = CascMtop<N, ME>;
+    constexpr uint32_t per_block = kCascWaves * U::GPW;
+    ca.nub = (ca.units + per_block - 1) / per_block;
+    const uint32_t blocks = ca.nub + ca.W * M::PB;
+    const uint32_t uw = U::planes_words + kCascWaves * U::tr_words;
+    const size_t lds = (size_t)(uw > M::words ? uw : M::words) * sizeof(uint64_t);
+    hipLaunchKernelGGL((k_cascade<N, ME, 10, CHECK>), dim3(blocks), dim3(64 * kCascWaves), lds, st, ca);
+    return hipGetLastError();
 }
 
 template <int N, int ME, int DIAG = 0, bool CHECK = false, bool LAT = false>
@@ -1273,11 +1497,11 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
         ca.snd_off[k] = (uint32_t)g.sender_off[k];
     ca.members = a.members;
     uint64_t off = 0;
-    const uint64_t per_word = cascade_scratch_words_per_word(g);
+    const uint64_t per_word = cascade_scratch_words_per_word(g, job.co);
     for (uint32_t k = 1; k + 2 <= g.me; ++k) {
         ca.R[k] = scratch + off;
         if (job.check) ca.tag[k] = scratch + W * per_word + off;
-        off += W * casc_level_words((int)g.L, (int)k);
+        off += W * casc_level_words((int)g.L, (int)k, job.co && k + 2 == g.me);
     }
     ca.epoch = job.epoch & 0xffffffffull;
     ca.inject = job.check == 2 ? 1u : 0u;
@@ -1328,6 +1552,17 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
     }
         BA_CASC_RANGE_SHAPES(BA_CASC_ROOT_LAUNCH)
 #undef BA_CASC_ROOT_LAUNCH
+        return hipErrorInvalidValue;
+    }
+    if (job.co) {  // one launch: units + co-resident fan-in blocks (whole tree, me >= 4)
+        if (job.h != 0 || g.me < 4) return hipErrorInvalidValue;
+        ProfScope ps(a.prof, "k_cascade_co", a.stream);
+#define BA_CASC_CO_LAUNCH(nn, mm)                                                         \
+    if (g.n == nn && g.me == mm)                                                        \
+        return job.check ? launch_cascade_co<nn, mm, true>(ca, a.stream)                \
+                         : launch_cascade_co<nn, mm>(ca, a.stream);
+        BA_CASC_TWO_SHAPES(BA_CASC_CO_LAUNCH)
+#undef BA_CASC_CO_LAUNCH
         return hipErrorInvalidValue;
     }
     if (job.two && g.me >= 4 && (job.h == 0 || cascade_range_two_supported(g, job.h))) {

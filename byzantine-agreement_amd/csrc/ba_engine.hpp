@@ -160,6 +160,7 @@ struct CascJob {
     const uint64_t* vin = nullptr;  // root mode: every unit's level-root_h votes (k_cascade_root)
     uint32_t root_h = 0;
     bool two = false;               // two launches: units, then the fan-in (k_cascade_top)
+    bool co = false;                // one launch: units + co-resident fan-in blocks (whole tree, me >= 4)
     uint32_t check = 0;           // tests: 1 = epoch tags checked, 2 = and one stale tag injected
     uint64_t epoch = 0;           // check: this launch's tag
 };
@@ -168,7 +169,7 @@ bool cascade_check_supported(const Geometry& g);
 bool cascade_range_supported(const Geometry& g, uint32_t h);
 bool cascade_range_two_supported(const Geometry& g, uint32_t h);
 uint64_t cascade_counters_per_word(const Geometry& g);       // 128-B counters per trial word
-uint64_t cascade_scratch_words_per_word(const Geometry& g);  // R_1..R_{me-2} words per trial word (x2 with check tags)
+uint64_t cascade_scratch_words_per_word(const Geometry& g, bool co = false);  // R_1..R_{me-2} words per trial word (x2 with check tags)
 bool cascade_root_pass_uses_scratch();                       // false: k_cascade_wtop (the default)
 hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_sender,
                           uint64_t* scratch, uint32_t* d_cnt, uint64_t trial0, uint64_t ntrials,

@@ -201,6 +201,7 @@ def test_two_launch_equals_one_launch(engine, monkeypatch, n, m, B):
     out = {}
     for two in ("1", "0"):
         monkeypatch.setenv("BA_CASC_TWO", two)
+        monkeypatch.setenv("BA_CASC_CO", "0")
         engine.profile(True)
         out[two] = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
         prof = engine.profile_read()
@@ -215,12 +216,56 @@ def test_two_launch_equals_one_launch(engine, monkeypatch, n, m, B):
         _check(a, n, m, B, **kw)
 
 
+CO_SHAPES = [(16, 5), (16, 4), (9, 4), (8, 5)]  # ba_cascade.hip BA_CASC_TWO_SHAPES
+
+
+@pytest.mark.parametrize("n,m", CO_SHAPES)
+@pytest.mark.parametrize("B", [1, 64, 70, 128])
+def test_co_launch_equals_two_launch(engine, monkeypatch, n, m, B):
+    """The CO launch (units + co-resident fan-in blocks polling the units'
+    granules, casc_co_top; the default up to 2 words) and the two-launch cascade
+    (units, then k_cascade_mtop) give the same bits, and the oracle's; the profile
+    shows which ran."""
+    from ba_amd import lib as L
+    kw = dict(seed=0xC0 + B + n, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1, order_mode=L.ORDER_RANDOM,
+              first_trial=64 * 5)
+    out = {}
+    for co in ("1", "0"):
+        monkeypatch.setenv("BA_CASC_CO", co)
+        engine.profile(True)
+        out[co] = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
+        prof = engine.profile_read()
+        engine.profile(False)
+        assert ("k_cascade_co" in prof) == (co == "1") and ("k_cascade_mtop" in prof) == (co == "0"), prof
+    monkeypatch.delenv("BA_CASC_CO")
+    engine.profile(True)
+    engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
+    assert "k_cascade_co" in engine.profile_read()  # the default at <= 2 words
+    engine.profile(False)
+    same(out["1"].decisions, out["0"].decisions, "decisions")
+    same(out["1"].outcome, out["0"].outcome, "outcome")
+    assert out["1"].counters == out["0"].counters
+    _check(out["1"], n, m, B, **kw)
+
+
+def test_co_launch_handoff_tags(engine, monkeypatch):
+    """The CO launch in the check build, 60 calls alternating batch 1 and 128 (new
+    inputs each): every granule the fan-in blocks accept carries this launch's
+    tag (0 mismatches), and replays never see the previous launch's granules."""
+    monkeypatch.setenv("BA_CASC_CO", "1")
+    monkeypatch.setenv("BA_CASC_CHECK", "1")
+    mism, cnt, _ = _check_calls(engine, 16, 5, (1, 128), 60, 1)
+    assert int(mism.sum()) == 0
+    assert (cnt[:, 0] > 0).all()
+
+
 @pytest.mark.parametrize("mtop", ["1", "0"])
 def test_two_launch_handoff_tags(engine, monkeypatch, mtop):
     """The two-launch mode in the check build: the fan-in launch reads every child
     the units launch wrote with this call's epoch (60 calls, batch 1024 and 512),
     fan-in by k_cascade_mtop and by k_cascade_top."""
     monkeypatch.setenv("BA_CASC_TWO", "1")
+    monkeypatch.setenv("BA_CASC_CO", "0")
     monkeypatch.setenv("BA_CASC_MTOP", mtop)
     monkeypatch.setenv("BA_CASC_CHECK", "1")
     mism, cnt, _ = _check_calls(engine, 16, 5, (1024, 512), 60, 1)
@@ -243,6 +288,7 @@ def test_fanin_variants_agree(engine, monkeypatch, n, m, B):
     kw = dict(seed=0x77 + B, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1, order_mode=L.ORDER_RANDOM,
               first_trial=64 * 4)
     monkeypatch.setenv("BA_CASC_TWO", "1")
+    monkeypatch.setenv("BA_CASC_CO", "0")
     out = {}
     for name, env in FANIN.items():
         for k, v in env.items():
@@ -271,6 +317,7 @@ def test_latency_mode_units_agree(engine, monkeypatch, n, m, B):
     kw = dict(seed=0x1A7 + B, faulty_mode=L.FAULTY_RANDOM, f=(n - 1) // 3 + 1, order_mode=L.ORDER_RANDOM,
               first_trial=64 * 11)
     monkeypatch.setenv("BA_CASC_TWO", "1")
+    monkeypatch.setenv("BA_CASC_CO", "0")
     out = {}
     for lat in ("1", "0"):
         monkeypatch.setenv("BA_CASC_LAT", lat)
@@ -290,6 +337,7 @@ def test_latency_mode_handoff_tags(engine, monkeypatch):
     """The latency-mode units in the check build: the fan-in reads every child with
     this call's epoch (40 calls, batch 1 and 64)."""
     monkeypatch.setenv("BA_CASC_TWO", "1")
+    monkeypatch.setenv("BA_CASC_CO", "0")
     monkeypatch.setenv("BA_CASC_LAT", "1")
     monkeypatch.setenv("BA_CASC_CHECK", "1")
     mism, cnt, _ = _check_calls(engine, 16, 5, (1, 64), 40, 1)
@@ -309,7 +357,9 @@ def _fuzz_cases(k=24, seed=0xF022):
         fanin = list(FANIN)[int(rng.integers(len(FANIN)))]
         fanin += "+lat" if rng.integers(2) else ""
         out.append((i, n, m, B, mode, two, fanin, int(rng.integers(0, 50)), int(rng.integers(1 << 30))))
-    return out
+    # the CO launch (units + co-resident fan-in blocks) drawn per case too
+    co = np.random.default_rng(seed + 1).integers(2, size=k)
+    return [c[:5] + (c[5] + ("+co" if co[j] else ""),) + c[6:] for j, c in enumerate(out)]
 
 
 @pytest.mark.parametrize("i,n,m,B,mode,two,fanin,ft,sd", _fuzz_cases())
@@ -320,7 +370,8 @@ def test_cascade_fuzz_vs_oracle(engine, monkeypatch, i, n, m, B, mode, two, fani
     (BA_CASC_TWO), the two-launch fan-in by any of the three kernels: bit-exact with the
     oracle on decisions, outcome bytes and counters."""
     from ba_amd import lib as L
-    monkeypatch.setenv("BA_CASC_TWO", two)
+    monkeypatch.setenv("BA_CASC_TWO", two.split("+")[0])
+    monkeypatch.setenv("BA_CASC_CO", "1" if two.endswith("+co") else "0")
     for k, v in FANIN[fanin.split("+")[0]].items():
         monkeypatch.setenv(k, v)
     monkeypatch.setenv("BA_CASC_LAT", "1" if fanin.endswith("+lat") else "0")

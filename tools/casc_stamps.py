@@ -40,7 +40,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--co", action="store_true",
+                    help="one CO launch (BA_CASC_CO=1): the fan-in blocks' rows follow the units blocks'")
     a = ap.parse_args()
+    if a.co:
+        os.environ["BA_CASC_CO"] = "1"
     n, m, B = 16, 5, a.batch
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -101,8 +105,11 @@ def main():
     mb = np.zeros((1 << 16, 16), np.uint64)
     assert lib.ba_lab_mtop_stamps_read(mb.ctypes.data, mb.nbytes) == 0
     blocks = W * 15
-    mt = mb[:blocks].astype(np.int64)
-    mph = ["kids+inputs+draws", "barrier1", "stepQ", "barrier2", "relay_q1", "store", "drain", "arrive"]
+    nub = (units + 19) // 20 if a.co else 0  # CO: the fan-in blocks follow the units blocks
+    mt = mb[nub:nub + blocks].astype(np.int64)
+    mph = (["draws+inputs", "barrier", "poll_units", "stepQ+barrier", "relay_q1_apply", "store", "drain",
+            "arrive"] if a.co else
+           ["kids+inputs+draws", "barrier1", "stepQ", "barrier2", "relay_q1", "store", "drain", "arrive"])
     md = np.diff(mt[:, :9], axis=1)
     lastb = mt[:, 11] != 0
     root = {}
@@ -118,7 +125,12 @@ def main():
             "gap_units_last_exit_to_mtop_last_entry_us": round(float((mt[:, 14].max() - rt1.max()) / 100.0), 2),
             "mtop_span_us": round(float((mt[:, 15].max() - mt[:, 14].min()) / 100.0), 2),
             "units_first_entry_to_mtop_last_exit_us": round(float((mt[:, 15].max() - rt0.min()) / 100.0), 2)}
-    print(json.dumps({"mtop": mtop,
+    if a.co:  # the wait: wave 0's children all fresh (s_memrealtime) vs the units' last exit
+        mtop["co_wait_done_minus_units_last_exit_us"] = {
+            "min": round(float((mt[:, 12].min() - rt1.max()) / 100.0), 2),
+            "max": round(float((mt[:, 12].max() - rt1.max()) / 100.0), 2)}
+        mtop["co_granule_polls"] = {"mean": float(mt[:, 13].mean()), "max": int(mt[:, 13].max())}
+    print(json.dumps({"mtop": mtop, "co": a.co,
         "batch": B, "units": units, "waves": int(waves), "active_waves": int(act.sum()),
         "us_per_call_stamped_lib": round(us_call, 2), "units_launch_span_us": round(float(span_us), 2),
         "wave_life_us": {"mean": round(float(life_us.mean()), 2), "p50": round(float(np.median(life_us)), 2),
