@@ -974,6 +974,16 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM4W_BLOCKS_PER_CU) void k_om4w(
     uint64_t* img = lds + (uint64_t)wv * G::words;
     const uint64_t total_words = (batch + 63) / 64;
     const uint64_t ntasks = (total_words + W - 1) / W;
+    // lane-derived values once per wave (k_om3w forms them per task; here that
+    // measured 3% slower with staged inputs: profiles/r05n_om4w_lane_ab.log)
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lw_ = lane / C2, la = lane - lw_ * C2;
+    const bool act = lane < (uint32_t)G::LANES;
+    const uint32_t lw = act ? lw_ : 0;
+    // member a of lane la's leaf block is E2[a + (a >= la)]; member d's R3T row
+    // is d + (d >= la) (the k_om3w tables, E2 in place of E, C2 in place of C + 1)
+    const LaneBytes<S> mem([la](int a) { return 8u * (a + ((uint32_t)a >= la ? 1u : 0u)); });
+    const LaneBytes<S> r3o([la](int d) { return (uint32_t)d >= la ? 8u * C2 : 0u; });
     uint64_t folded = 0;  // run counters folded per task (wave_fold)
     // tasks: the first wave-round static, then (sk.tasks != nullptr: a persistent
     // launch) each further task from the launch's atomic counter, fetched at the
@@ -983,16 +993,6 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM4W_BLOCKS_PER_CU) void k_om4w(
     // one wave for the rest of the launch
     const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
     for (uint64_t task = (uint64_t)blockIdx.x * wpb + wv; task < ntasks;) {
-        // lane-derived values per task, from mbcnt (as k_om3w: none live across tasks)
-        uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-        asm volatile("" : "+v"(lane));
-        const uint32_t lw_ = lane / C2, la = lane - lw_ * C2;
-        const bool act = lane < (uint32_t)G::LANES;
-        const uint32_t lw = act ? lw_ : 0;
-        // member a of lane la's leaf block is E2[a + (a >= la)]; member d's R3T row
-        // is d + (d >= la) (the k_om3w tables, E2 in place of E, C2 in place of C + 1)
-        const LaneBytes<S> mem([la](int a) { return 8u * (a + ((uint32_t)a >= la ? 1u : 0u)); });
-        const LaneBytes<S> r3o([la](int d) { return (uint32_t)d >= la ? 8u * C2 : 0u; });
         uint32_t next_raw = 0;
         if (sk.tasks != nullptr && lane == 0) next_raw = atomicAdd(sk.tasks, 1u);
         const uint64_t w0 = task * W;
@@ -1123,7 +1123,7 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM4W_BLOCKS_PER_CU) void k_om4w(
         __builtin_amdgcn_wave_barrier();
         task = sk.tasks != nullptr ? nwaves + __builtin_amdgcn_readfirstlane(next_raw) : task + nwaves;
     }
-    wave_flush_folded(folded, threadIdx.x & 63, wv, wpb, counters, sk, false);
+    wave_flush_folded(folded, lane, wv, wpb, counters, sk, false);
 }
 
 // WAVE engine launch: one wave per W-word task, 4 independent waves per block,

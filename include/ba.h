@@ -121,7 +121,18 @@ typedef struct ba_params {
 #define BA_C_FAULTY_TOTAL 10   /* sum of f over trials                               */
 #define BA_C_ATTACK_DECISIONS 11 /* lieutenant decisions == attack                   */
 /* Slot 14 is test-only: hand-off tag mismatches counted by the LEVELS cascade's
- * check build (environment BA_CASC_CHECK=1, read per call; 0 on a correct run).
+ * check build (environment BA_CASC_CHECK=1, read per call; 0 on a correct run),
+ * and in every build a granule hand-off that stayed stale past its bounded poll
+ * (never on a correct run).
+ * The cascade's in-launch hand-offs between workgroups rest on gfx950 / ROCm 7.2
+ * behaviour measured in MI355X_MICROARCH.md, not on the HIP memory model:
+ * granules ({32-bit value half, 32-bit launch tag} in one aligned 8-byte sc1
+ * store, read with sc1 loads and re-read until the tag matches: the guide's R2
+ * form, observed untorn) for R_1 and, in CO launches, R_{me-2}; drained sc1
+ * stores + a relaxed agent-scope counter add + sc1 loads (the guide's
+ * valid-forms row 1) only in the one-launch cascade and the non-default wave
+ * fan-in (BA_CASC_MTOP=0). The check build and its
+ * tests (tests/test_gpu_cascade.py, part of the GPU suite) watch both.
  * Slot 15 is the multi-GPU entries' error flag (always 0 in returned counters). */
 #define BA_C_CHECK_MISMATCH 14
 

@@ -132,18 +132,22 @@ def test_writelane_check_catches_missing_nop(tmp_path):
 
 # VGPR spill budgets of the shipped kernels (scratch traffic: each spilled VGPR is
 # a 256-B store + load per wave where it is spilled).  The bench's kernel
-# k_om3w<10, staged> and every cascade kernel must not spill at all; the other
-# WAVE instantiations are held at what they compile to now (round 5: lane-derived
-# values formed per task from mbcnt, so none is live across the task loop).
+# k_om3w<10, staged> and every cascade kernel must not spill at all (round 5:
+# k_om3w forms its lane-derived values per task from mbcnt, so none is live
+# across the task loop); k_om4w keeps them per wave -- its allocation then spills
+# more, outside the round loop, and config 3 runs faster (8.67e8 vs 8.51e8
+# staged trials/s, profiles/r05n_om4w_lane_ab.log) -- and is held at what it
+# compiles to now.
 SPILL_BUDGET = [  # (symbol regex, max VGPR spills)
     (r"_ZN2ba6k_om3wILi10ELi0ELb1E", 0),   # the bench kernel (BASELINE config 2)
     (r"_ZN2ba6k_om3wILi9ELi0ELb1E", 1),
     (r"_ZN2ba6k_om3w", 0),
-    (r"_ZN2ba6k_om4wILi13ELb1E", 3),      # config 3 (staged)
-    (r"_ZN2ba6k_om4wILi13ELb0E", 8),      # config 3 (inputs in-kernel)
-    (r"_ZN2ba6k_om4wILi1[01]ELb", 1),
-    (r"_ZN2ba6k_om4wILi12ELb", 29),
-    (r"_ZN2ba6k_om4wILi14ELb", 48),
+    (r"_ZN2ba6k_om4wILi13ELb1E", 21),     # config 3 (staged)
+    (r"_ZN2ba6k_om4wILi13ELb0E", 29),     # config 3 (inputs in-kernel)
+    (r"_ZN2ba6k_om4wILi1[01]ELb", 26),
+    (r"_ZN2ba6k_om4wILi12ELb", 61),
+    (r"_ZN2ba6k_om4wILi14ELb", 82),
+    (r"_ZN2ba6k_om4wILi[6-9]ELb", 44),
     (r"_ZN2ba6k_om4w", 0),
     (r"_ZN2ba\d+k_cascade", 0),            # config 5 (units, fan-in, root pass)
 ]
