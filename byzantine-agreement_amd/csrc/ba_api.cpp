@@ -606,7 +606,7 @@ static bool use_cascade(ba_ctx* ctx, const Geometry& g) {
 }
 
 constexpr uint64_t kCascTwoWords = 1;
-constexpr uint64_t kCascCoWords = 2;
+constexpr uint64_t kCascCoWords = 8;
 
 // BA_CASC_CHECK (tests only, read per call): 1 = the cascade's check build
 // (epoch tags beside every hand-off word, mismatches counted into
