@@ -65,11 +65,6 @@ for s in $STAGES; do
     configs) run configs 600 python -u tools/run_configs.py || exit $? ;;
     c5) run c5_1024 300 python -u tools/config5_prof.py --batch 1024 --split || exit $?
         run c5_1 300 python -u tools/config5_prof.py --batch 1 --reps 500 --split || exit $? ;;
-    c5ab) for r in 1 2; do for lib in byzantine-agreement_amd/ba_amd/libba_hip.so ab/libba_noacq.so; do
-            t=$(basename $lib .so)_$r
-            run c5ab_1024_$t 300 env BA_HIP_LIB=$ROOT/$lib python -u tools/config5_prof.py --batch 1024 || exit $?
-            run c5ab_1_$t 300 env BA_HIP_LIB=$ROOT/$lib python -u tools/config5_prof.py --batch 1 --reps 500 || exit $?
-          done; done ;;
     multirank) run pytest_multirank 900 python -u -m pytest tests/test_multirank_gpu.py tests/test_dist.py -m gpu -v --timeout 420 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
     casc) run pytest_casc 600 python -u -m pytest tests/test_gpu_cascade.py tests/test_dist.py -m gpu -v --timeout 200 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
     c5prof) for b in 1024 1; do
