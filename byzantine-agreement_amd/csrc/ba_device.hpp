@@ -508,6 +508,19 @@ __device__ __forceinline__ uint64_t part1by1(uint32_t v) {
     return x;
 }
 
+// Sum of x over the wave's 64 lanes (uniform result): DPP within each 16-lane
+// row (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror: four VALU
+// adds), then the four row sums by readlane -- where a __shfl_xor tree is six
+// dependent ds_bpermute round trips through LDS.
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 0) + (uint32_t)__builtin_amdgcn_readlane((int)x, 16) +
+           (uint32_t)__builtin_amdgcn_readlane((int)x, 32) + (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
+}
+
 struct TrialCounts {
     uint32_t v[C_NUM];
     __device__ __forceinline__ TrialCounts() {

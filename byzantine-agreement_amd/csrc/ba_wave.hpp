@@ -467,9 +467,7 @@ __device__ __forceinline__ void wave_epilogue(uint64_t* in0, const uint64_t* au0
 __device__ __forceinline__ void wave_fold(const TrialCounts& tc, uint32_t lane, uint64_t& mine) {
 #pragma unroll
     for (int c = 0; c < C_NUM; ++c) {
-        uint32_t x = tc.v[c];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+        const uint32_t x = wave_sum_u32(tc.v[c]);
         if (lane == (uint32_t)c) mine += x;
     }
 }
