@@ -95,35 +95,41 @@ def main():
                         "floor_us_2w": round(calls / peaks.get(2, max(peaks.values())) * 1e6, 2),
                         "peak_source": bench.PHILOX_PEAK_SRC},
            "counters_one_call": one, "lib_sha16": bench.so_digest()}
-    # two calls in flight: call i on ctx i % 2 (each ctx on its own stream, own
-    # outputs), one HIP-event pair bracketing all of them on the first stream
-    eng2 = L.Engine(0)
-    st2 = torch.cuda.ExternalStream(eng2.stream(), device=dev)
-    dec2 = torch.empty(B, dtype=torch.int64, device=dev)
-    out2 = torch.empty(B, dtype=torch.uint8, device=dev)
+    # k calls in flight (k = 2, 3): call i on ctx i % k (each ctx on its own stream,
+    # own outputs), one HIP-event pair bracketing all of them on the first stream
+    for k, name in ((2, "two"), (3, "three")):
+        extra = [L.Engine(0) for _ in range(k - 1)]
+        sts = [st] + [torch.cuda.ExternalStream(e.stream(), device=dev) for e in extra]
+        decs = [dec] + [torch.empty(B, dtype=torch.int64, device=dev) for _ in extra]
+        outs = [out] + [torch.empty(B, dtype=torch.uint8, device=dev) for _ in extra]
+        engs = [eng] + extra
 
-    def call2(i):
-        if i % 2 == 0:
-            call()
-        else:
-            eng2.run_device(pg, B, d_faulty=fb.data_ptr(), d_order=ob.data_ptr(),
-                            d_decisions=dec2.data_ptr(), d_outcome=out2.data_ptr(),
-                            d_counters=cnt.data_ptr(), stream=st2.cuda_stream)
-    for i in range(20):
-        call2(i)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
-    st2.wait_event(e0)
-    for i in range(a.reps):
-        call2(i)
-    st.wait_stream(st2)
-    e1.record(st)
-    torch.cuda.synchronize()
-    sec2 = e0.elapsed_time(e1) * 1e-3 / a.reps
-    rec["us_per_call_two_in_flight"] = round(sec2 * 1e6, 2)
-    rec["instances_per_s_two_in_flight"] = round(B / sec2, 1)
-    eng2.close()
+        def callk(i):
+            j = i % k
+            if j == 0:
+                call()
+            else:
+                engs[j].run_device(pg, B, d_faulty=fb.data_ptr(), d_order=ob.data_ptr(),
+                                   d_decisions=decs[j].data_ptr(), d_outcome=outs[j].data_ptr(),
+                                   d_counters=cnt.data_ptr(), stream=sts[j].cuda_stream)
+        for i in range(20):
+            callk(i)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for x in sts[1:]:
+            x.wait_event(e0)
+        for i in range(a.reps):
+            callk(i)
+        for x in sts[1:]:
+            st.wait_stream(x)
+        e1.record(st)
+        torch.cuda.synchronize()
+        seck = e0.elapsed_time(e1) * 1e-3 / a.reps
+        rec[f"us_per_call_{name}_in_flight"] = round(seck * 1e6, 2)
+        rec[f"instances_per_s_{name}_in_flight"] = round(B / seck, 1)
+        for e in extra:
+            e.close()
     print(json.dumps(rec), flush=True)
 
     if a.split:
