@@ -606,7 +606,7 @@ static bool use_cascade(ba_ctx* ctx, const Geometry& g) {
 }
 
 constexpr uint64_t kCascTwoWords = 1;
-constexpr uint64_t kCascCoWords = 8;
+constexpr uint64_t kCascCoWords = 4;
 
 // BA_CASC_CHECK (tests only, read per call): 1 = the cascade's check build
 // (epoch tags beside every hand-off word, mismatches counted into
@@ -640,6 +640,10 @@ static int run_cascade(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge, CascJob job 
     // The whole tree as ONE launch of units + co-resident fan-in blocks (no
     // units -> fan-in kernel boundary; ba_cascade.hip casc_co_top) up to
     // kCascCoWords 64-trial words.  BA_CASC_CO=0/1 (read per call) forces it.
+    // The limit also bounds the launch's polling fan-in blocks (15 per word at
+    // n=16, m=5: 60): forward progress needs the polling blocks of all CO
+    // launches running at once to leave block slots for their units (768 at 3
+    // blocks per CU), so a dozen such launches may run concurrently.
     if (job.two && job.h == 0) {
         const char* e = getenv("BA_CASC_CO");
         job.co = e ? atoi(e) != 0 : (a.batch + 63) / 64 <= kCascCoWords;

@@ -223,7 +223,7 @@ CO_SHAPES = [(16, 5), (16, 4), (9, 4), (8, 5)]  # ba_cascade.hip BA_CASC_TWO_SHA
 @pytest.mark.parametrize("B", [1, 64, 70, 128])
 def test_co_launch_equals_two_launch(engine, monkeypatch, n, m, B):
     """The CO launch (units + co-resident fan-in blocks polling the units'
-    granules, casc_co_top; the default up to 8 words) and the two-launch cascade
+    granules, casc_co_top; the default up to 4 words) and the two-launch cascade
     (units, then k_cascade_mtop) give the same bits, and the oracle's; the profile
     shows which ran."""
     from ba_amd import lib as L
@@ -240,7 +240,7 @@ def test_co_launch_equals_two_launch(engine, monkeypatch, n, m, B):
     monkeypatch.delenv("BA_CASC_CO")
     engine.profile(True)
     engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
-    assert "k_cascade_co" in engine.profile_read()  # the default at <= 8 words
+    assert "k_cascade_co" in engine.profile_read()  # the default at <= 4 words
     engine.profile(False)
     same(out["1"].decisions, out["0"].decisions, "decisions")
     same(out["1"].outcome, out["0"].outcome, "outcome")

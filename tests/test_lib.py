@@ -145,8 +145,8 @@ SPILL_BUDGET = [  # (symbol regex, max VGPR spills)
     (r"_ZN2ba6k_om4wILi13ELb1E", 21),     # config 3 (staged)
     (r"_ZN2ba6k_om4wILi13ELb0E", 29),     # config 3 (inputs in-kernel)
     (r"_ZN2ba6k_om4wILi1[01]ELb", 26),
-    (r"_ZN2ba6k_om4wILi12ELb", 61),
-    (r"_ZN2ba6k_om4wILi14ELb", 82),
+    (r"_ZN2ba6k_om4wILi12ELb", 62),
+    (r"_ZN2ba6k_om4wILi14ELb", 88),
     (r"_ZN2ba6k_om4wILi[6-9]ELb", 44),
     (r"_ZN2ba6k_om4w", 0),
     (r"_ZN2ba\d+k_cascade", 0),            # config 5 (units, fan-in, root pass)
