@@ -50,6 +50,8 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--split", action="store_true")
+    ap.add_argument("--no-inflight", action="store_true",
+                    help="calls on one stream only (clean per-kernel rocprofv3 averages)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -97,7 +99,7 @@ def main():
            "counters_one_call": one, "lib_sha16": bench.so_digest()}
     # k calls in flight (k = 2, 3): call i on ctx i % k (each ctx on its own stream,
     # own outputs), one HIP-event pair bracketing all of them on the first stream
-    for k, name in ((2, "two"), (3, "three")):
+    for k, name in (() if a.no_inflight else ((2, "two"), (3, "three"))):
         extra = [L.Engine(0) for _ in range(k - 1)]
         sts = [st] + [torch.cuda.ExternalStream(e.stream(), device=dev) for e in extra]
         decs = [dec] + [torch.empty(B, dtype=torch.int64, device=dev) for _ in extra]

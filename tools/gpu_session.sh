@@ -70,7 +70,7 @@ for s in $STAGES; do
     c5prof) for b in 1024 1; do
           (cd /tmp && export TMPDIR=/tmp && mkdir -p "$ROOT/gpurun_out/c5prof_$b" && \
            timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/c5prof_$b" -o run -- \
-             python3 "$ROOT/tools/config5_prof.py" --batch $b --reps 300 > "$ROOT/gpurun_out/c5prof_$b.log" 2>&1); rc=$?
+             python3 "$ROOT/tools/config5_prof.py" --batch $b --reps 300 --no-inflight > "$ROOT/gpurun_out/c5prof_$b.log" 2>&1); rc=$?
           echo "c5prof $b rc=$rc" | tee -a gpurun_out/steps.log; [ $rc -eq 0 ] || exit $rc; done ;;
     c5pmc) C5="$ROOT/tools/config5_prof.py --batch 1024 --reps 50"
          for pass in "sq:SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
