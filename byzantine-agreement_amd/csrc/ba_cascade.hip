@@ -457,7 +457,13 @@ __device__ __forceinline__ uint64_t relay_slots(const CascArgs& a, const uint64_
 // consumer in.  The consumer then zeroes the granules it read, so a replayed
 // launch (a captured graph repeats its epoch argument) never sees an old tag;
 // the tag is never 0.
-constexpr uint32_t kGranuleSpinCap = 1u << 16;  // s_sleep 1 polls before giving up (~ms)
+// Every poll of a granule is bounded in time (s_memrealtime, 100 MHz): 2 s in
+// the product -- long enough that a launch descheduled by another process's
+// work is not taken for a lost hand-off -- and 200 ms in the check build, whose
+// stale-tag injection waits out the bound once per launch.  A granule still
+// stale at the bound (never in a correct run) is counted into slot 14.
+template <bool CHECK>
+constexpr uint64_t casc_wait_ticks() { return CHECK ? 20000000ull : 200000000ull; }
 __device__ __forceinline__ uint32_t casc_gtag(uint64_t epoch) { return ((uint32_t)epoch << 1) | 1u; }
 
 // A relay value computed ahead of its step (CO fan-in blocks), or none.
@@ -609,7 +615,8 @@ __device__ __forceinline__ void casc_root_step(const CascArgs& a, const uint64_t
         return ok;
     };
     bool ok = fresh();
-    for (uint32_t spin = 0; !__all(ok) && spin < kGranuleSpinCap; ++spin) {  // wave-uniform
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (!__all(ok) && __builtin_amdgcn_s_memrealtime() - t0 <= casc_wait_ticks<CHECK>()) {  // wave-uniform
         __builtin_amdgcn_s_sleep(1);
         static_for<0, K - 1>([&](auto jj) {
             g0[jj()] = act ? load_sc1(gp[jj()]) : 0ull;
@@ -617,7 +624,7 @@ __device__ __forceinline__ void casc_root_step(const CascArgs& a, const uint64_t
         });
         ok = fresh();
     }
-    // a granule still stale at the cap: never in a correct run.  Counted into
+    // a granule still stale at the bound: never in a correct run.  Counted into
     // slot 14 (BA_C_CHECK_MISMATCH) so tests see it -- per stale lane in CHECK
     // builds (their stale-tag injection expects exactly one), once per wave
     // otherwise
@@ -740,12 +747,11 @@ struct CascMtop {
 // {value half, epoch tag} in one 8-B sc1 store (MI355X_MICROARCH.md's R2 form),
 // so the units neither drain nor count -- until every lane's carry this launch's
 // tag, and zeroes them for the next launch (each granule has one reader).  The
-// poll is bounded (kCoWaitTicks of s_memrealtime; a granule still stale then is
+// poll is bounded (casc_wait_ticks of s_memrealtime; a granule still stale then is
 // counted into BA_C_CHECK_MISMATCH).  Forward progress needs no dispatch order:
 // a polling block waits only for units blocks, which wait for nothing, and the
 // polling blocks of a launch (W * PB: 15 per word at n=16, m=5) are far fewer
 // than the chip's block slots.
-constexpr uint64_t kCoWaitTicks = 20000000;  // s_memrealtime (100 MHz): 200 ms
 
 template <int N, int ME, bool CHECK>
 __device__ __forceinline__ void casc_co_top(const CascArgs& a, uint64_t* lds, uint32_t bid) {
@@ -837,7 +843,7 @@ __device__ __forceinline__ void casc_co_top(const CascArgs& a, uint64_t* lds, ui
     load_all();
     bool ok = fresh();
     while (!__all(ok)) {  // wave-uniform
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kCoWaitTicks) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > casc_wait_ticks<CHECK>()) break;
         __builtin_amdgcn_s_sleep(2);
         load_all();
         ok = fresh();
