@@ -248,6 +248,21 @@ def test_co_launch_equals_two_launch(engine, monkeypatch, n, m, B):
     _check(out["1"], n, m, B, **kw)
 
 
+@pytest.mark.parametrize("B,co", [(255, True), (256, True), (257, False), (320, False)])
+def test_co_launch_limit(engine, B, co):
+    """The CO launch is the default up to 4 words (256 instances) and the two-launch
+    cascade above; both sides of the limit equal the oracle (the sliced port)."""
+    from ba_amd import lib as L
+    n, m = 16, 5
+    kw = dict(seed=0x11A7 + B, faulty_mode=L.FAULTY_RANDOM, f=5, order_mode=L.ORDER_RANDOM, first_trial=64 * 2)
+    engine.profile(True)
+    res = engine.run(n, m, B, engine=L.ENGINE_LEVELS, **kw)
+    prof = engine.profile_read()
+    engine.profile(False)
+    assert ("k_cascade_co" in prof) == co and ("k_cascade_mtop" in prof) == (not co), prof
+    _check(res, n, m, B, **kw)
+
+
 def test_co_launch_handoff_tags(engine, monkeypatch):
     """The CO launch in the check build, 60 calls alternating batch 1 and 128 (new
     inputs each): every granule the fan-in blocks accept carries this launch's
