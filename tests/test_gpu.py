@@ -434,9 +434,15 @@ def test_om4_wave_vs_oracle(monkeypatch, n, m, f):
 
 def test_random_configs_fuzz(engine):
     """30 seeded random (n, m, f, modes, batch, first_trial) cases on the AUTO
-    engine, each bit-exact against the oracle (decisions, outcomes, counters)."""
+    engine, each bit-exact against the oracle (decisions, outcomes, counters).
+    BA_FUZZ_SEED="s1,s2,..." draws 30 per seed instead (a wider sweep on a lease;
+    the default seed is the one the round-end run uses)."""
     from ba_amd import lib as L
-    rng = np.random.default_rng(20261016)
+    for s in os.environ.get("BA_FUZZ_SEED", "20261016").split(","):
+        _random_configs(L, engine, np.random.default_rng(int(s)), s)
+
+
+def _random_configs(L, engine, rng, s):
     for case in range(30):
         n = int(rng.integers(2, 17))
         m = int(rng.integers(0, 5))
@@ -460,7 +466,7 @@ def test_random_configs_fuzz(engine):
             kw.update(order_mode=omode, order_value=int(rng.integers(0, 3)))
         od, oo, ocnt = oracle_c.run(n, m, B, **kw)
         res = engine.run(n, m, B, **kw)
-        tag = f"case {case}: n={n} m={m} B={B} fmode={fmode} omode={omode} f={f}"
+        tag = f"seed {s} case {case}: n={n} m={m} B={B} fmode={fmode} omode={omode} f={f}"
         same(res.decisions, od, "decisions " + tag)
         same(res.outcome, oo, "outcome " + tag)
         assert {k: res.counters[k] for k in ocnt} == ocnt, tag

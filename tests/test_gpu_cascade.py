@@ -5,6 +5,8 @@ C oracle on decisions, outcome bytes and counters, for every instantiated
 (n, m_eff) shape, ragged batches, given and drawn inputs, several chunks per
 call; and identical to the multi-launch LEVELS pipeline it replaces
 (BA_NO_CASCADE=1, read per call)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -360,7 +362,12 @@ def test_latency_mode_handoff_tags(engine, monkeypatch):
     assert (cnt[:, 0] > 0).all()
 
 
-def _fuzz_cases(k=24, seed=0xF022):
+def _fuzz_cases(k=24, seed=None):
+    # BA_FUZZ_SEED="s1,s2,..." draws k cases per seed instead (a wider sweep on a lease)
+    if seed is None:
+        seeds = os.environ.get("BA_FUZZ_SEED", str(0xF022)).split(",")
+        return [c for j, s in enumerate(seeds)
+                for c in ((i + j * k,) + c[1:] for i, c in enumerate(_fuzz_cases(k, int(s))))]
     rng = np.random.default_rng(seed)
     shapes = SHAPES
     out = []
