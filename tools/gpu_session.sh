@@ -72,6 +72,26 @@ for s in $STAGES; do
            timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/c5prof_$b" -o run -- \
              python3 "$ROOT/tools/config5_prof.py" --batch $b --reps 300 --no-inflight > "$ROOT/gpurun_out/c5prof_$b.log" 2>&1); rc=$?
           echo "c5prof $b rc=$rc" | tee -a gpurun_out/steps.log; [ $rc -eq 0 ] || exit $rc; done ;;
+    c3) run config3 300 python -u tools/config3_prof.py || exit $? ;;
+    c3prof) for md in staged inkernel; do
+          (cd /tmp && export TMPDIR=/tmp && mkdir -p "$ROOT/gpurun_out/c3prof_$md" && \
+           timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/c3prof_$md" -o run -- \
+             python3 "$ROOT/tools/config3_prof.py" --mode $md --reps 20 > "$ROOT/gpurun_out/c3prof_$md.log" 2>&1); rc=$?
+          echo "c3prof $md rc=$rc" | tee -a gpurun_out/steps.log; [ $rc -eq 0 ] || exit $rc; done ;;
+    c3pmc) for md in staged inkernel; do
+         C3="$ROOT/tools/config3_prof.py --mode $md --reps 3"
+         for pass in "sq:SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
+                     "lds:SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
+                     "fetch:FETCH_SIZE GRBM_GUI_ACTIVE GRBM_COUNT" "write:WRITE_SIZE"; do
+           name=${pass%%:*}; ctrs=${pass#*:}
+           (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $ctrs --output-format csv \
+              -d "$ROOT/gpurun_out/c3pmc_$md" -o "$name" -- python3 $C3 > "$ROOT/gpurun_out/c3pmc_${md}_$name.log" 2>&1)
+           rc=$?; echo "c3pmc $md $name rc=$rc" | tee -a gpurun_out/steps.log; [ $rc -eq 0 ] || exit $rc
+         done
+         python3 tools/pmc_summary.py gpurun_out/c3pmc_$md gpurun_out/c3pmc_${md}_summary.json \
+           --workload "tools/config3_prof.py --mode $md: n=13 m=4, 8388608 trials per launch" \
+           --config 13,4,8388608,auto/$md,k_om4w > gpurun_out/c3pmc_${md}_summary.log 2>&1
+       done ;;
     c5pmc) C5="$ROOT/tools/config5_prof.py --batch 1024 --reps 50"
          for pass in "sq:SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
                      "lds:SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
