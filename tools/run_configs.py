@@ -235,6 +235,29 @@ def main():
             rec["seconds_staged"] = sdt
             rec["staged_note"] = ("inputs staged in HBM before timing (as bench.py), one "
                                   "ba_run_trials_device call; counters equal the in-kernel run")
+            # one rank's share at N=8 (8,388,608 trials, the launch the committed
+            # rocprofv3 trace and PMC of k_om4w<13> cover: tools/config3_prof.py),
+            # timed with HIP events over back-to-back calls on one stream, and its
+            # three rooflines from the same-build PMC
+            import config3_prof
+            T8 = min(T, 8 << 20)
+            sc.zero_()
+
+            def call8():
+                eng.run_device(pg, T8, d_faulty=fb.data_ptr(), d_order=ob.data_ptr(),
+                               d_decisions=sd.data_ptr(), d_outcome=so.data_ptr(),
+                               d_counters=sc.data_ptr(), stream=st.cuda_stream)
+            call8()
+            torch.cuda.synchronize(dev)
+            s8 = config3_prof.ev_time(call8, 10, torch.cuda.ExternalStream(st.cuda_stream, device=dev))
+            roof, valu, comp = config3_prof.rooflines(n, m, T8, s8, True, engine="auto/staged")
+            rec["rank_share_trials"] = T8
+            rec["rank_share_us_per_call"] = round(s8 * 1e6, 2)
+            rec["rank_share_trials_per_s"] = T8 / s8
+            rec["roofline"], rec["valu_roofline"], rec["compute_roofline"] = roof, valu, comp
+            rec["roofline_note"] = (f"one k_om4w<13> launch over {T8} staged trials (one rank's share "
+                                    "of 64M at N=8), HIP events; traffic / VALU from the committed "
+                                    "PMC of the same build (same_build)")
             del fb, ob, sd, so
         out.append(rec)
 
