@@ -186,7 +186,10 @@ class InstanceSplitGraphs:
 
     def replay(self):
         """One split call; returns (decisions, outcome, counters) (reused tensors).
-        Ordered after the caller's current stream and before its later work."""
+        Ordered after the caller's current stream and before its later work.
+        Asynchronous: after synchronizing, L.check_handoff(counters) (a lost
+        in-launch hand-off makes the call's results invalid; a graph replays its
+        launch's epoch, so after such an error the graphs must be rebuilt)."""
         if self.g_root is None:  # one graph, replayed on the caller's current stream
             self.g_tree.replay()
             return self.dec, self.out, self.cnt

@@ -176,6 +176,24 @@ def _check(lib, rc: int):
         raise BAError(rc, lib.ba_last_error().decode())
 
 
+C_HANDOFF_LOST = 14  # BA_C_CHECK_MISMATCH: a cascade hand-off poll ran out of time
+
+
+def check_handoff(counters):
+    """Raise BAError(EDEVICE) if a device-path call's counters (16 int64: a torch
+    tensor, numpy array, list or COUNTER dict with "CHECK_MISMATCH") carry a lost
+    in-launch hand-off (slot 14, include/ba.h): that call's results are invalid.
+    ba_run_trials and the multi-rank jobs check it themselves; callers of the
+    asynchronous *_device entry points check it after their synchronize."""
+    if isinstance(counters, dict):
+        v = int(counters.get("CHECK_MISMATCH", 0))
+    else:
+        v = int(counters[C_HANDOFF_LOST])
+    if v != 0:
+        raise BAError(EDEVICE, f"in-launch hand-off timed out ({v} stale granule poll(s), counter "
+                               f"slot {C_HANDOFF_LOST}); results invalid")
+
+
 def effective_depth(n: int, m: int) -> int:
     return min(m, n - 2) if n >= 2 else 0
 
@@ -283,7 +301,8 @@ class Engine:
 
     def run_device(self, params: Params, batch: int, d_faulty=0, d_order=0, d_table=0, d_poll=0,
                    d_decisions=0, d_outcome=0, d_counters=0, stream=0):
-        """Enqueue on device pointers (ints, e.g. torch tensor .data_ptr()); asynchronous."""
+        """Enqueue on device pointers (ints, e.g. torch tensor .data_ptr()); asynchronous.
+        After synchronizing, check the counters with check_handoff (include/ba.h)."""
         _check(self.lib, self.lib.ba_run_trials_device(
             self.handle, ctypes.byref(params), batch, d_faulty or None, d_order or None,
             d_table or None, d_poll or None, d_decisions or None, d_outcome or None,

@@ -9,9 +9,12 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/ba.h"
 #include "ba_engine.hpp"
@@ -228,7 +231,22 @@ struct ba_ctx {
     hipEvent_t last_ev = nullptr;
     hipStream_t last_stream = nullptr;
     bool have_last = false;
+    // CO cascade launches of this ctx that may still run (co_admit): the
+    // stream of the last one and the polling blocks of the largest since the
+    // stream was last seen idle.  Guarded by co_registry().mu.
+    hipStream_t co_stream = nullptr;
+    uint64_t co_pending = 0;
 };
+
+// Every live ctx, for the CO launch admission (co_admit).
+struct CoRegistry {
+    std::mutex mu;
+    std::vector<ba_ctx*> ctxs;
+};
+static CoRegistry& co_registry() {
+    static CoRegistry r;
+    return r;
+}
 
 // A call about to use the ctx's scratch / sink on stream `s` first waits for
 // the ctx's previous call if that ran on another stream (include/ba.h: calls of
@@ -372,6 +390,10 @@ extern "C" int ba_ctx_create(int device, ba_ctx** out) {
         delete ctx;
         return fail(BA_ENOMEM, "counter sink allocation failed");
     }
+    {
+        std::lock_guard<std::mutex> lk(co_registry().mu);
+        co_registry().ctxs.push_back(ctx);
+    }
     *out = ctx;
     return BA_OK;
 }
@@ -410,6 +432,11 @@ extern "C" int ba_ctx_stream(ba_ctx* ctx, void** stream) {
 
 extern "C" void ba_ctx_destroy(ba_ctx* ctx) {
     if (!ctx) return;
+    {
+        std::lock_guard<std::mutex> lk(co_registry().mu);
+        auto& v = co_registry().ctxs;
+        v.erase(std::remove(v.begin(), v.end(), ctx), v.end());
+    }
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     prof_collect(ctx);
@@ -622,6 +649,64 @@ static uint32_t cascade_check_mode(const Geometry& g) {
 // scratch shrinks with the rank's unit range (internal, never returned)
 constexpr int kCascadeNoFit = 1;
 
+// CO launch admission.  A CO launch's fan-in blocks spin on granules; at me = 5
+// the word's s0 = 0 block also waits for sibling fan-in blocks dispatched after
+// it (ba_cascade.hip, casc_co_top), which need free block slots.  So the polling
+// blocks of all CO launches that may run at once on a device are bounded by
+// half the chip's block slots at the kernel's occupancy (3 blocks per CU): a
+// call over the bound takes the two-launch cascade instead, whatever
+// BA_CASC_CO says.  "May run at once": calls of one ctx are ordered (ctx_order),
+// so a ctx contributes the largest CO launch it queued since its stream was
+// last seen idle (hipStreamQuery: host-side, nothing is added to any stream);
+// other ctxs' CO launches (other threads, other streams) count until their
+// stream drains.  Launches captured into graphs are not counted (their replays
+// are the caller's to schedule, include/ba.h).  Per process: other processes
+// sharing the GPU are not seen -- a poll that still times out is an error,
+// never a wrong answer (BA_EDEVICE, handoff_lost).
+// BA_TEST_CO_BUDGET (tests only, read per call) replaces the bound.
+static uint64_t co_poll_budget(const ba_ctx* ctx) {
+    if (const char* e = getenv("BA_TEST_CO_BUDGET")) return strtoull(e, nullptr, 0);
+    return (uint64_t)ctx->cu_count * 3 / 2;
+}
+
+static bool co_admit(ba_ctx* ctx, hipStream_t s, uint64_t pollers) {
+    const uint64_t budget = co_poll_budget(ctx);
+    if (pollers > budget) return false;
+    if (stream_capturing(s)) return true;
+    std::lock_guard<std::mutex> lk(co_registry().mu);
+    uint64_t busy = 0;
+    for (ba_ctx* c : co_registry().ctxs) {
+        if (c == ctx || c->device != ctx->device || c->co_pending == 0) continue;
+        // a stream being captured may not be queried: its launches count
+        if (!stream_capturing(c->co_stream) && hipStreamQuery(c->co_stream) == hipSuccess) {
+            c->co_pending = 0;
+            continue;
+        }
+        busy += c->co_pending;
+    }
+    return busy + pollers <= budget;
+}
+
+static void co_note(ba_ctx* ctx, hipStream_t s, uint64_t pollers) {
+    if (stream_capturing(s)) return;
+    std::lock_guard<std::mutex> lk(co_registry().mu);
+    ctx->co_pending = std::max(ctx->co_pending, pollers);  // the previous ones finish first
+    ctx->co_stream = s;
+}
+
+// The polling (fan-in) blocks of a CO launch over W words: one per level-(me-5)
+// slot of every word (k_cascade_mtop's shape, CascMtop::PB)
+static uint64_t co_pollers(const Geometry& g, uint64_t words) {
+    return words * (g.me >= 5 ? g.S[g.me - 5] : 1u);
+}
+
+// A poll of a cascade hand-off that ran out of time (ba_cascade.hip) leaves a
+// non-zero BA_C_CHECK_MISMATCH: the launch's results are invalid.
+static int handoff_lost(uint64_t n) {
+    return fail(BA_EDEVICE, "in-launch hand-off timed out (%llu stale granule poll(s), counter slot "
+                "%d); results invalid", (unsigned long long)n, BA_C_CHECK_MISMATCH);
+}
+
 // job.h != 0 (the subtree split): one chunk (`whole`), no counters.
 static int run_cascade(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge, CascJob job = CascJob{}) {
     const Geometry& g = ge->g;
@@ -657,6 +742,9 @@ static int run_cascade(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge, CascJob job 
                                       (job.check ? 2 : 1) + cascade_counters_per_word(g) * 128;
         if (ctx->scratch_budget / co_bytes < (a.batch + 63) / 64) job.co = false;
     }
+    const uint64_t pollers = co_pollers(g, (a.batch + 63) / 64);
+    if (job.co && !co_admit(ctx, a.stream, pollers)) job.co = false;  // forward progress bound
+    if (const char* e = getenv("BA_TEST_GRANULE_TICKS")) job.wait_ticks = strtoull(e, nullptr, 0);
     const uint64_t r_bytes = uses ? cascade_scratch_words_per_word(g, job.co) * sizeof(uint64_t) *
                                         (job.check ? 2 : 1) : 0;
     const uint64_t c_bytes = uses ? cascade_counters_per_word(g) * 128 : 0;
@@ -691,6 +779,7 @@ static int run_cascade(ba_ctx* ctx, const RunArgs& a, GeoEntry* ge, CascJob job 
         job.epoch = ++ctx->casc_epoch;
         HIP_TRY(launch_cascade(a, g, (const uint8_t*)ge->sender.p, (uint64_t*)ctx->scratch.p,
                                (uint32_t*)ctx->casc.p, trial0, nt, job));
+        if (job.co) co_note(ctx, a.stream, pollers);
     }
     return BA_OK;
 }
@@ -993,7 +1082,10 @@ extern "C" int ba_run_trials(ba_ctx* ctx, const ba_params* p, uint64_t batch,
     if (rc != BA_OK) return rc;
     if (decisions) HIP_TRY(hipMemcpyAsync(decisions, ctx->io_dec.p, batch * 8, hipMemcpyDeviceToHost, st));
     if (outcome) HIP_TRY(hipMemcpyAsync(outcome, ctx->io_out.p, batch, hipMemcpyDeviceToHost, st));
-    if (counters) HIP_TRY(hipMemcpyAsync(counters->v, ctx->io_cnt.p, BA_NCOUNTERS * 8, hipMemcpyDeviceToHost, st));
+    uint64_t h_cnt[BA_NCOUNTERS];
+    HIP_TRY(hipMemcpyAsync(h_cnt, ctx->io_cnt.p, BA_NCOUNTERS * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    if (h_cnt[BA_C_CHECK_MISMATCH] != 0) return handoff_lost(h_cnt[BA_C_CHECK_MISMATCH]);
+    if (counters) memcpy(counters->v, h_cnt, sizeof h_cnt);
     return BA_OK;
 }

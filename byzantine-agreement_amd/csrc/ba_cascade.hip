@@ -106,6 +106,7 @@ struct CascArgs {
     uint64_t* tag[kCascMaxLevels];  // CHECK: the same layout, epoch tags
     uint64_t epoch;                 // CHECK: this launch's tag
     uint32_t inject;                // CHECK: 1 = unit 0 stores a stale tag (detector test)
+    uint64_t wait_ticks;            // bound of every granule poll (s_memrealtime ticks, 100 MHz)
     uint32_t* cnt;                // counters [..] x kCascCounterStride
     uint32_t cnt_off[kCascMaxLevels];  // level k (0..Q-1) counters of word w at cnt_off[k] + w*|L_k|;
                                        // cnt_off[Q]: the word's root counter at cnt_off[Q] + w
@@ -462,8 +463,12 @@ __device__ __forceinline__ uint64_t relay_slots(const CascArgs& a, const uint64_
 // work is not taken for a lost hand-off -- and 200 ms in the check build, whose
 // stale-tag injection waits out the bound once per launch.  A granule still
 // stale at the bound (never in a correct run) is counted into slot 14.
-template <bool CHECK>
-constexpr uint64_t casc_wait_ticks() { return CHECK ? 20000000ull : 200000000ull; }
+// The bound is a launch argument (CascArgs::wait_ticks): kCascWaitTicks, or
+// kCascWaitTicksCheck in the check build; BA_TEST_GRANULE_TICKS (tests only)
+// shrinks it so a launch times out.  A timed-out launch's results are invalid,
+// and every host entry point that reads the counters back returns BA_EDEVICE
+// for it (ba_api.cpp handoff_lost, ba_multi.cpp finish_job).
+constexpr uint64_t kCascWaitTicks = 200000000ull, kCascWaitTicksCheck = 20000000ull;
 __device__ __forceinline__ uint32_t casc_gtag(uint64_t epoch) { return ((uint32_t)epoch << 1) | 1u; }
 
 // A relay value computed ahead of its step (CO fan-in blocks), or none.
@@ -616,7 +621,7 @@ __device__ __forceinline__ void casc_root_step(const CascArgs& a, const uint64_t
     };
     bool ok = fresh();
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (!__all(ok) && __builtin_amdgcn_s_memrealtime() - t0 <= casc_wait_ticks<CHECK>()) {  // wave-uniform
+    while (!__all(ok) && __builtin_amdgcn_s_memrealtime() - t0 <= a.wait_ticks) {  // wave-uniform
         __builtin_amdgcn_s_sleep(1);
         static_for<0, K - 1>([&](auto jj) {
             g0[jj()] = act ? load_sc1(gp[jj()]) : 0ull;
@@ -747,11 +752,17 @@ struct CascMtop {
 // {value half, epoch tag} in one 8-B sc1 store (MI355X_MICROARCH.md's R2 form),
 // so the units neither drain nor count -- until every lane's carry this launch's
 // tag, and zeroes them for the next launch (each granule has one reader).  The
-// poll is bounded (casc_wait_ticks of s_memrealtime; a granule still stale then is
-// counted into BA_C_CHECK_MISMATCH).  Forward progress needs no dispatch order:
-// a polling block waits only for units blocks, which wait for nothing, and the
-// polling blocks of a launch (W * PB: 15 per word at n=16, m=5) are far fewer
-// than the chip's block slots.
+// poll is bounded (a.wait_ticks of s_memrealtime; a granule still stale then is
+// counted into BA_C_CHECK_MISMATCH, which the host turns into BA_EDEVICE).
+// Forward progress rests on two things:
+//  - in-order dispatch of one launch's blocks: the units blocks (which wait for
+//    nothing) hold their slots before any fan-in block of the launch is placed;
+//  - at me = 5 (PB > 1) the word's s0 = 0 fan-in block also polls the R_1
+//    granules of its siblings s0 = 1..PB-1, which have HIGHER block indices: they
+//    must find slots while s0 = 0 spins.  The host bounds the polling blocks of
+//    all CO launches in flight on a device (ba_api.cpp co_admit: at most half
+//    the chip's block slots), so slots stay free for them; past the bound a
+//    call takes the two-launch cascade.
 
 template <int N, int ME, bool CHECK>
 __device__ __forceinline__ void casc_co_top(const CascArgs& a, uint64_t* lds, uint32_t bid) {
@@ -843,7 +854,7 @@ __device__ __forceinline__ void casc_co_top(const CascArgs& a, uint64_t* lds, ui
     load_all();
     bool ok = fresh();
     while (!__all(ok)) {  // wave-uniform
-        if (__builtin_amdgcn_s_memrealtime() - t0 > casc_wait_ticks<CHECK>()) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > a.wait_ticks) break;
         __builtin_amdgcn_s_sleep(2);
         load_all();
         ok = fresh();
@@ -1511,6 +1522,7 @@ hipError_t launch_cascade(const RunArgs& a, const Geometry& g, const uint8_t* d_
     }
     ca.epoch = job.epoch & 0xffffffffull;
     ca.inject = job.check == 2 ? 1u : 0u;
+    ca.wait_ticks = job.wait_ticks ? job.wait_ticks : job.check ? kCascWaitTicksCheck : kCascWaitTicks;
     ca.cnt = d_cnt;
     uint32_t coff = 0;
     for (uint32_t k = 0; k + 3 < g.me; ++k) {

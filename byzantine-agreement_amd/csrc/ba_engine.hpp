@@ -163,6 +163,7 @@ struct CascJob {
     bool co = false;                // one launch: units + co-resident fan-in blocks (whole tree, me >= 4)
     uint32_t check = 0;           // tests: 1 = epoch tags checked, 2 = and one stale tag injected
     uint64_t epoch = 0;           // check: this launch's tag
+    uint64_t wait_ticks = 0;      // granule poll bound (0: the default; BA_TEST_GRANULE_TICKS)
 };
 bool cascade_supported(const Geometry& g);
 bool cascade_check_supported(const Geometry& g);

@@ -16,9 +16,10 @@
 //    wrap step's mt[1]) and once more in lockstep with the mixing sweep, so
 //    nothing of it is stored;
 //  * the mixed state goes to HBM once, i-major ([624][T]: every step of a wave
-//    is one coalesced 256-B access), and the outputs twist it lazily in place,
-//    in index order -- exactly CPython's twist, for as many outputs (and twists)
-//    as the round draws;
+//    is one coalesced 256-B access) -- only the positions the round's outputs
+//    will read (a window sized per wave, k_mt_table) -- and the outputs twist it
+//    lazily in place, in index order -- exactly CPython's twist, for as many
+//    outputs (and twists) as the round draws;
 //  * a coin is the first output whose top two bits are < 2 (randint(0, 1) =
 //    _randbelow(2)), bit 30 = 0 meaning "attack".
 #include "ba_leaf.hpp"  // static_for
@@ -62,72 +63,50 @@ __device__ __forceinline__ uint32_t om1_coins(uint32_t n, uint32_t m, uint32_t f
     return c;
 }
 
-__global__ __launch_bounds__(256) void k_mt_table(uint32_t n, uint32_t m, uint64_t T,
-                                                  const uint64_t* __restrict__ seeds,
-                                                  const uint32_t* __restrict__ faulty,
-                                                  const uint32_t* __restrict__ poll, uint32_t stride,
-                                                  uint32_t* __restrict__ table,
-                                                  uint32_t* __restrict__ next_word,
-                                                  uint32_t* __restrict__ st) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= T) return;
-    // random.seed(seed): key = the 32-bit limbs of |seed| (one zero limb for 0)
-    const uint64_t seed = seeds[t];
-    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-    const bool two = k1 != 0;
-    // key sweep step at index i adds key[j] + j, j = (i - 1) % len
-    const uint32_t add_even = k0, add_odd = two ? k1 + 1u : k0;
-    // 1. the key sweep to its end: p1 = mt[1] after its first step, a = mt[623]
-    uint32_t a = kMtInit.v[0], p1 = 0;
-    for (int i = 1; i < kMtN; ++i) {
-        a = (kMtInit.v[i] ^ ((a ^ (a >> 30)) * 1664525u)) + (((i - 1) & 1) ? add_odd : add_even);
-        if (i == 1) p1 = a;
-    }
-    // its 624th step wraps to i = 1 (mt[0] = mt[623], j = 623 % len)
-    const uint32_t p1w = (p1 ^ ((a ^ (a >> 30)) * 1664525u)) + add_odd;
-    // 2. the mixing sweep, i = 2 .. 623, with the key sweep's mt[i] recomputed
-    //    alongside; then its wrap step for mt[1], and mt[0] = 0x80000000
-    uint32_t c1 = p1, c2 = p1w;
-    for (int i = 2; i < kMtN; ++i) {
-        c1 = (kMtInit.v[i] ^ ((c1 ^ (c1 >> 30)) * 1664525u)) + (((i - 1) & 1) ? add_odd : add_even);
-        c2 = (c1 ^ ((c2 ^ (c2 >> 30)) * 1566083941u)) - (uint32_t)i;
-        st[(uint64_t)i * T + t] = c2;
-    }
-    st[T + t] = (p1w ^ ((c2 ^ (c2 >> 30)) * 1566083941u)) - 1u;
-    st[t] = 0x80000000u;
-    // 3. the round's coins from lazily twisted outputs (CPython's twist is an
-    //    in-place sweep in index order: new[i] reads mt[i], mt[i+1], mt[i+397],
-    //    the last two already new where they wrapped -- so is this), in blocks
-    //    of kBlk outputs: the 2*kBlk+1 state words a block reads are loaded
-    //    together (each output's source lies 227 or more positions behind any
-    //    output of its own block), the lanes of a wave at the same positions
-    //    (coalesced), for as long as any lane still draws
+// Draw the round's coins (and the next word) from the state stored at the
+// slots `slot(i)` maps state positions to, twisting lazily in place: output k
+// reads positions k, k+1 and k+397 (mod 624; a position below k+397-624 is
+// already new, as in CPython's in-place twist).  `lim` = the number of outputs
+// the stored positions allow (a window), or 0 for the full state (any number,
+// second twists included: positions wrap).  Returns false if the lane needed
+// more than `lim` outputs (it then starts over on the full state).
+template <typename Slot>
+__device__ __forceinline__ bool mt_draw(uint32_t* __restrict__ st, uint64_t T, uint64_t t, Slot slot,
+                                        uint32_t lim, uint32_t cnt, bool want_next, uint32_t* row,
+                                        uint32_t* __restrict__ next_word) {
     constexpr uint32_t kBlk = 16;
-    const uint32_t cnt = om1_coins(n, m, faulty[t], poll ? poll[t] : 0u);
-    uint32_t* row = table + t * stride;
-    const bool want_next = next_word != nullptr;
     uint32_t pos = 0, c = 0, word = 0;
-    bool done = !want_next && cnt == 0;
+    bool done = !want_next && cnt == 0, ok = true;
     while (__any(!done)) {
+        if (!done && lim != 0 && pos >= lim) {  // the window is used up: the slow path
+            done = true;
+            ok = false;
+        }
         if (!done) {
+            // every lane still drawing is at the same position: row addresses
+            // are wave-uniform (scalar), the lane's column its offset
+            const uint32_t upos = (uint32_t)__builtin_amdgcn_readfirstlane((int)pos);
+            uint32_t* col = st + t;
+            auto at = [&](uint32_t i) { return col + (uint64_t)slot(i) * T; };
             uint32_t cur[kBlk + 1], far[kBlk];
             static_for<0, kBlk + 1>([&](auto k) {
-                uint32_t i = pos + k();
+                uint32_t i = upos + k();
                 i = i >= (uint32_t)kMtN ? i - kMtN : i;
-                cur[k()] = st[(uint64_t)i * T + t];
+                cur[k()] = *at(i);
             });
             static_for<0, kBlk>([&](auto k) {
-                uint32_t i = pos + k() + kMtM;
+                uint32_t i = upos + k() + kMtM;
                 i = i >= (uint32_t)kMtN ? i - kMtN : i;
                 i = i >= (uint32_t)kMtN ? i - kMtN : i;
-                far[k()] = st[(uint64_t)i * T + t];
+                far[k()] = *at(i);
             });
             static_for<0, kBlk>([&](auto k) {
-                uint32_t i = pos + k();
+                uint32_t i = upos + k();
                 i = i >= (uint32_t)kMtN ? i - kMtN : i;
                 const uint32_t y = (cur[k()] & 0x80000000u) | (cur[k() + 1] & 0x7fffffffu);
                 const uint32_t v = far[k()] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-                st[(uint64_t)i * T + t] = v;
+                // in place, where a later output reads it (its k + 397 wraps here)
+                if (lim == 0 || i + (kMtN - kMtM) < lim) *at(i) = v;
                 const uint32_t out = mt_temper(v);
                 if (c < cnt) {
                     const uint32_t r = out >> 30;  // randint(0, 1): top two bits, retried >= 2
@@ -149,7 +128,122 @@ __global__ __launch_bounds__(256) void k_mt_table(uint32_t n, uint32_t m, uint64
             pos = pos >= (uint32_t)kMtN ? pos - kMtN : pos;
         }
     }
-    if (cnt & 31) row[cnt >> 5] = word;
+    if (ok && (cnt & 31)) row[cnt >> 5] = word;
+    return ok;
+}
+
+// CPython init_by_array's two recurrences (key sweep, mixing sweep)
+__device__ __forceinline__ uint32_t mt_key_step(uint32_t init_i, uint32_t a, uint32_t add) {
+    return (init_i ^ ((a ^ (a >> 30)) * 1664525u)) + add;
+}
+__device__ __forceinline__ uint32_t mt_mix_step(uint32_t c1, uint32_t c2, uint32_t i) {
+    return (c1 ^ ((c2 ^ (c2 >> 30)) * 1566083941u)) - i;
+}
+
+// Mixing-sweep steps i in [i0, i1) (uniform bounds), the key sweep's mt[i]
+// recomputed alongside; STORE: mt[i] to *p, p advancing one row (T words) per
+// step.  Unrolled so the constant table's scalar loads go out in groups.
+template <bool STORE>
+__device__ __forceinline__ void mt_mix_range(uint32_t i0, uint32_t i1, uint32_t& c1, uint32_t& c2,
+                                             uint32_t add_even, uint32_t add_odd, uint32_t*& p,
+                                             uint64_t T) {
+#pragma unroll 8
+    for (uint32_t i = i0; i < i1; ++i) {
+        c1 = mt_key_step(kMtInit.v[i], c1, ((i - 1) & 1) ? add_odd : add_even);
+        c2 = mt_mix_step(c1, c2, i);
+        if constexpr (STORE) {
+            *p = c2;
+            p += T;
+        }
+    }
+}
+
+// random.seed(seed)'s state (init_by_array, CPython), storing positions
+// [2, lo_end) at rows 2.. and [397, 397 + hi) at rows from lo_end on (rows of
+// T words from st0 = the lane's column), positions 1 and 0 at rows 1 and 0.
+// lo_end = 624, hi = 0: the full state, row = position.  The key sweep is a
+// recurrence over i whose values the mixing sweep needs again, index by index:
+// it is run once to its end (for mt[623] and the wrap step's mt[1]) and once
+// more in lockstep with the mixing sweep, so nothing of it is stored.
+__device__ __forceinline__ void mt_seed(uint32_t* st0, uint64_t T, uint64_t seed, uint32_t lo_end,
+                                        uint32_t hi) {
+    // random.seed(seed): key = the 32-bit limbs of |seed| (one zero limb for 0)
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    const bool two = k1 != 0;
+    // key sweep step at index i adds key[j] + j, j = (i - 1) % len
+    const uint32_t add_even = k0, add_odd = two ? k1 + 1u : k0;
+    // 1. the key sweep to its end: p1 = mt[1] after its first step, a = mt[623]
+    const uint32_t p1 = mt_key_step(kMtInit.v[1], kMtInit.v[0], add_even);
+    uint32_t a = p1;
+#pragma unroll 8
+    for (uint32_t i = 2; i < (uint32_t)kMtN; ++i) a = mt_key_step(kMtInit.v[i], a, ((i - 1) & 1) ? add_odd : add_even);
+    // its 624th step wraps to i = 1 (mt[0] = mt[623], j = 623 % len)
+    const uint32_t p1w = (p1 ^ ((a ^ (a >> 30)) * 1664525u)) + add_odd;
+    // 2. the mixing sweep, i = 2 .. 623; then its wrap step for mt[1], and
+    //    mt[0] = 0x80000000
+    uint32_t c1 = p1, c2 = p1w;
+    uint32_t* p = st0 + 2 * T;
+    if (hi == 0) {  // the full state
+        mt_mix_range<true>(2u, (uint32_t)kMtN, c1, c2, add_even, add_odd, p, T);
+    } else {
+        mt_mix_range<true>(2u, lo_end, c1, c2, add_even, add_odd, p, T);
+        mt_mix_range<false>(lo_end, (uint32_t)kMtM, c1, c2, add_even, add_odd, p, T);
+        mt_mix_range<true>((uint32_t)kMtM, (uint32_t)kMtM + hi, c1, c2, add_even, add_odd, p, T);
+        mt_mix_range<false>((uint32_t)kMtM + hi, (uint32_t)kMtN, c1, c2, add_even, add_odd, p, T);
+    }
+    st0[T] = (p1w ^ ((c2 ^ (c2 >> 30)) * 1566083941u)) - 1u;
+    st0[0] = 0x80000000u;
+}
+
+// One thread per trial.  The state goes to HBM [slot][T] (every step of a wave
+// one coalesced 256-B access), but only the positions the round's outputs read
+// (round 6: the whole 624-word state was written, 2.5 KB per trial, and the
+// kernel was bound by those writes): a round of D <= 227 outputs reads
+// positions 0..D and 397..397+D-1, and a few more past 227 (the in-place twist
+// reads its own new words there).  Each wave sizes its window from its lanes'
+// coin counts (om1_coins): Wv = max over the wave of 2.5 cnt + 16 (+1 for the
+// next word; a coin takes 2 outputs on average, so that is > 4 sigma of
+// retries), rounded to the draw block.  A lane that still needs more outputs
+// starts over on its full 624-word state (positions = slots), as does every
+// lane of a wave whose window would not fit in 624 slots.
+__global__ __launch_bounds__(256) void k_mt_table(uint32_t n, uint32_t m, uint64_t T,
+                                                  const uint64_t* __restrict__ seeds,
+                                                  const uint32_t* __restrict__ faulty,
+                                                  const uint32_t* __restrict__ poll, uint32_t stride,
+                                                  uint32_t* __restrict__ table,
+                                                  uint32_t* __restrict__ next_word,
+                                                  uint32_t* __restrict__ st) {
+    constexpr uint32_t kBlk = 16, kFar = kMtN - kMtM;  // 227 outputs before a wrap
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = t < T;
+    const bool want_next = next_word != nullptr;
+    const uint32_t cnt = live ? om1_coins(n, m, faulty[t], poll ? poll[t] : 0u) : 0u;
+    uint32_t need = (!live || (cnt == 0 && !want_next)) ? 0u : 2u * cnt + cnt / 2u + 16u + (want_next ? 1u : 0u);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) need = max(need, (uint32_t)__shfl_xor((int)need, off, 64));
+    if (!live) return;
+    // the wave-uniform window (outputs)
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)((need + kBlk - 1) / kBlk * kBlk));
+    uint32_t* row = table + t * stride;
+    const uint64_t seed = seeds[t];
+    uint32_t* col = st + t;
+    bool ok = true;
+    if (wv == 0) {
+        // no lane of the wave draws: random.seed's state is never read
+    } else if (wv < (uint32_t)kMtM) {
+        // window: positions 0..wv at rows 0..wv, 397..397+min(wv,227)-1 after them
+        // (below 624 rows; outputs past 227 read positions <= wv back as new)
+        const uint32_t hi = wv < kFar ? wv : kFar;
+        mt_seed(col, T, seed, wv + 1, hi);
+        auto slot = [wv](uint32_t i) { return i <= wv ? i : wv + 1u + (i - (uint32_t)kMtM); };
+        ok = mt_draw(st, T, t, slot, wv, cnt, want_next, row, next_word);
+    } else {
+        ok = false;
+    }
+    if (!ok) {  // the full state: every position at its own row, any number of outputs
+        mt_seed(col, T, seed, (uint32_t)kMtN, 0u);
+        (void)mt_draw(st, T, t, [](uint32_t i) { return i; }, 0u, cnt, want_next, row, next_word);
+    }
     for (uint32_t wi = (cnt + 31) >> 5; wi < stride; ++wi) row[wi] = 0;  // the row's unused words
 }
 

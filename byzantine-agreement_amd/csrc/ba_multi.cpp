@@ -42,10 +42,12 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 
 #include "../../include/ba.h"
 
@@ -135,18 +137,39 @@ struct ba_comm {
     size_t votes_bytes = 0;
     hipStream_t stream = nullptr;  // the ctx's own stream (not owned: the ctx outlives the comm)
     uint64_t* h_pin = nullptr;  // pinned host words: counter read-back, flag upload / read-back
-    uint64_t timeout_ms = kDefaultTimeoutMs;  // watchdog of the blocking jobs
-    bool aborted = false;  // ncclCommAbort ran: the RCCL communicator is gone
+    std::atomic<uint64_t> timeout_ms{kDefaultTimeoutMs};  // watchdog of the blocking jobs
+    // ba_comm_abort may run on a supervisor thread while a job enqueues a
+    // collective: `mu` guards `comm` and `aborted` -- every collective is
+    // enqueued under it (with_comm), and the abort frees the communicator under
+    // it, so no enqueue ever sees a freed or null communicator, and only one
+    // thread ever calls ncclCommAbort
+    std::mutex mu;
+    std::atomic<bool> aborted{false};  // ncclCommAbort ran: the RCCL communicator is gone
+    // recorded on the stream right before a job's first collective: the
+    // watchdog's clock starts when the rank's own work ahead of it is done
+    // (comm_wait), so a long local step is never taken for a peer that left
+    hipEvent_t coll_ev = nullptr;
 };
 
 // Abort the RCCL communicator: this rank's pending collectives return (RCCL
 // kernels poll the abort flag), the communicator is freed, and every further
-// call on the comm fails with BA_EABORTED.
+// call on the comm fails with BA_EABORTED.  Safe from any thread.
 static void abort_comm(ba_comm* c) {
-    if (c->aborted) return;
-    c->aborted = true;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->aborted.load()) return;
     if (c->comm && rccl().h) (void)rccl().comm_abort(c->comm);
     c->comm = nullptr;
+    c->aborted.store(true);
+}
+
+// Enqueue a collective on the live communicator (under the comm's lock, so a
+// concurrent ba_comm_abort waits for the enqueue, and the enqueue never sees a
+// freed communicator); an aborted comm gives ncclInvalidUsage without a call.
+template <typename F>
+static ncclResult_t with_comm(ba_comm* c, F&& f) {
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->aborted.load() || !c->comm) return ncclInvalidUsage;
+    return f(c->comm);
 }
 
 static int fail_aborted(const ba_comm* c) {
@@ -154,10 +177,29 @@ static int fail_aborted(const ba_comm* c) {
                  "a new one", c->rank, c->nranks);
 }
 
+// After an abort: RCCL's kernels see the abort flag and return, so the stream
+// drains -- waited for at most this long (a hung kernel of the rank's own work
+// must not block the caller forever; the comm is unusable either way, and
+// ba_comm_destroy synchronizes the stream).
+constexpr uint64_t kAbortDrainMs = 10000;
+
+static void drain_after_abort(ba_comm* c) {
+    const uint64_t t0 = now_ns();
+    while (hipStreamQuery(c->stream) == hipErrorNotReady && now_ns() - t0 < kAbortDrainMs * 1000000ull) {
+        timespec ts = {0, 200000};
+        nanosleep(&ts, nullptr);
+    }
+}
+
 // Wait for the comm's stream (the blocking jobs' collectives): poll it, and
-// past the timeout abort the communicator so the stream drains, and fail.
+// past the timeout abort the communicator so the stream drains, and fail.  The
+// clock starts when coll_ev (recorded right before the job's first collective)
+// has completed: the rank's own kernels ahead of the collectives may take as
+// long as they take; only the exchange itself is timed.
 static int comm_wait(ba_comm* c, const char* what) {
-    const uint64_t t0 = now_ns(), lim = c->timeout_ms * 1000000ull;
+    const uint64_t lim = c->timeout_ms.load() * 1000000ull;
+    uint64_t t0 = 0;
+    bool timing = false;
     for (uint32_t k = 0;; ++k) {
         const hipError_t e = hipStreamQuery(c->stream);
         if (e == hipSuccess) return BA_OK;
@@ -165,18 +207,38 @@ static int comm_wait(ba_comm* c, const char* what) {
             abort_comm(c);
             return failf(BA_EDEVICE, "%s: %s (communicator aborted)", what, hipGetErrorString(e));
         }
-        if (now_ns() - t0 > lim) {
+        if (c->aborted.load()) {  // ba_comm_abort from another thread
+            drain_after_abort(c);
+            return failf(BA_EABORTED, "%s: communicator of rank %d aborted during the job", what,
+                         c->rank);
+        }
+        if (!timing) {
+            const hipError_t q = hipEventQuery(c->coll_ev);
+            if (q == hipSuccess) {
+                timing = true;
+                t0 = now_ns();
+            } else if (q != hipErrorNotReady) {
+                abort_comm(c);
+                return failf(BA_EDEVICE, "%s: %s (communicator aborted)", what, hipGetErrorString(q));
+            }
+        } else if (now_ns() - t0 > lim) {
             abort_comm(c);
-            (void)hipStreamSynchronize(c->stream);  // the aborted collectives return
+            drain_after_abort(c);  // the aborted collectives return
             return failf(BA_EABORTED, "%s: no completion within %llu ms (a peer left the "
                          "exchange); communicator of rank %d aborted", what,
-                         (unsigned long long)c->timeout_ms, c->rank);
+                         (unsigned long long)c->timeout_ms.load(), c->rank);
         }
         if (k > 2000) {  // a short spin first: most jobs complete within it
             timespec ts = {0, 50000};
             nanosleep(&ts, nullptr);
         }
     }
+}
+
+// Mark the start of the job's exchange (comm_wait's clock); a failed record
+// leaves the clock to start at once, which only shortens the watchdog.
+static void mark_exchange(ba_comm* c) {
+    if (hipEventRecord(c->coll_ev, c->stream) != hipSuccess) (void)hipEventRecord(c->coll_ev, nullptr);
 }
 
 // ba_api.cpp, library-internal
@@ -218,8 +280,10 @@ extern "C" int ba_comm_create(struct ba_ctx* ctx, int nranks, int rank,
         if (v > 0) c->timeout_ms = v;
     }
     if (hipMalloc(&c->d_cnt, BA_NCOUNTERS * sizeof(uint64_t)) != hipSuccess ||
-        hipHostMalloc(&c->h_pin, (BA_NCOUNTERS + 2) * sizeof(uint64_t), 0) != hipSuccess) {
+        hipHostMalloc(&c->h_pin, (BA_NCOUNTERS + 2) * sizeof(uint64_t), 0) != hipSuccess ||
+        hipEventCreateWithFlags(&c->coll_ev, hipEventDisableTiming) != hipSuccess) {
         if (c->d_cnt) (void)hipFree(c->d_cnt);
+        if (c->h_pin) (void)hipHostFree(c->h_pin);
         delete c;
         return failf(BA_ENOMEM, "communicator buffers");
     }
@@ -229,6 +293,7 @@ extern "C" int ba_comm_create(struct ba_ctx* ctx, int nranks, int rank,
     if (e != ncclSuccess) {
         (void)hipFree(c->d_cnt);
         (void)hipHostFree(c->h_pin);
+        (void)hipEventDestroy(c->coll_ev);
         delete c;
         return failf(BA_EDEVICE, "ncclCommInitRank(%d ranks, rank %d): %s", nranks, rank,
                      r.error_string(e));
@@ -241,7 +306,8 @@ extern "C" void ba_comm_destroy(struct ba_comm* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->comm && !c->aborted && rccl().h) (void)rccl().comm_destroy(c->comm);
+    if (c->comm && !c->aborted.load() && rccl().h) (void)rccl().comm_destroy(c->comm);
+    if (c->coll_ev) (void)hipEventDestroy(c->coll_ev);
     if (c->d_cnt) (void)hipFree(c->d_cnt);
     if (c->d_votes) (void)hipFree(c->d_votes);
     if (c->h_pin) (void)hipHostFree(c->h_pin);
@@ -257,7 +323,7 @@ extern "C" int ba_comm_rank(struct ba_comm* comm, int* nranks, int* rank) {
 
 extern "C" int ba_comm_set_timeout(struct ba_comm* comm, uint64_t timeout_ms) {
     if (!comm || timeout_ms == 0) return failf(BA_EINVAL, "comm is NULL or timeout is 0");
-    comm->timeout_ms = timeout_ms;
+    comm->timeout_ms.store(timeout_ms);
     return BA_OK;
 }
 
@@ -310,11 +376,14 @@ extern "C" int ba_split_share(uint32_t n, uint32_t m, uint32_t level, int nranks
 // ---------------------------------------------------------------------------
 extern "C" int ba_comm_allreduce_device(struct ba_comm* comm, uint64_t* d_counters, void* stream) {
     if (!comm || !d_counters) return failf(BA_EINVAL, "comm and d_counters are required");
-    if (comm->aborted) return fail_aborted(comm);
+    if (comm->aborted.load()) return fail_aborted(comm);
     if (hipSetDevice(comm->device) != hipSuccess) return failf(BA_EDEVICE, "hipSetDevice");
     Rccl& r = rccl();
-    const ncclResult_t e = r.all_reduce(d_counters, d_counters, BA_NCOUNTERS, ncclUint64, ncclSum,
-                                        comm->comm, (hipStream_t)stream);
+    const ncclResult_t e = with_comm(comm, [&](ncclComm_t cm) {
+        return r.all_reduce(d_counters, d_counters, BA_NCOUNTERS, ncclUint64, ncclSum, cm,
+                            (hipStream_t)stream);
+    });
+    if (comm->aborted.load()) return fail_aborted(comm);
     if (e != ncclSuccess) return failf(BA_EDEVICE, "ncclAllReduce: %s", r.error_string(e));
     return BA_OK;
 }
@@ -325,20 +394,24 @@ extern "C" int ba_comm_allgather_split_votes_device(struct ba_comm* comm, uint32
     if (!comm || !d_votes) return failf(BA_EINVAL, "comm and d_votes are required");
     const uint64_t units = ba_split_units(n, m, level);
     if (units == 0) return failf(BA_EINVAL, "no level-%u split votes for n=%u, m=%u", level, n, m);
-    if (comm->aborted) return fail_aborted(comm);
+    if (comm->aborted.load()) return fail_aborted(comm);
     if (hipSetDevice(comm->device) != hipSuccess) return failf(BA_EDEVICE, "hipSetDevice");
     const uint64_t W = (batch + 63) / 64, row = (uint64_t)(n - 1 - level) * W;  // words per unit
     Rccl& r = rccl();
-    ncclResult_t e = r.group_start();
-    for (int q = 0; q < comm->nranks && e == ncclSuccess; ++q) {
-        uint32_t ub = 0, ue = 0;
-        (void)ba_split_share(n, m, level, comm->nranks, q, &ub, &ue);
-        if (ue == ub) continue;
-        uint64_t* part = d_votes + (uint64_t)ub * row;  // rank q's rows, in place on every rank
-        e = r.broadcast(part, part, (size_t)(ue - ub) * row, ncclUint64, q, comm->comm,
-                        (hipStream_t)stream);
-    }
-    const ncclResult_t e2 = r.group_end();
+    ncclResult_t e2 = ncclSuccess;
+    const ncclResult_t e = with_comm(comm, [&](ncclComm_t cm) {
+        ncclResult_t eb = r.group_start();
+        for (int q = 0; q < comm->nranks && eb == ncclSuccess; ++q) {
+            uint32_t ub = 0, ue = 0;
+            (void)ba_split_share(n, m, level, comm->nranks, q, &ub, &ue);
+            if (ue == ub) continue;
+            uint64_t* part = d_votes + (uint64_t)ub * row;  // rank q's rows, in place on every rank
+            eb = r.broadcast(part, part, (size_t)(ue - ub) * row, ncclUint64, q, cm, (hipStream_t)stream);
+        }
+        e2 = r.group_end();
+        return eb;
+    });
+    if (comm->aborted.load()) return fail_aborted(comm);
     if (e != ncclSuccess || e2 != ncclSuccess)
         return failf(BA_EDEVICE, "vote all-gather (grouped ncclBroadcast): %s",
                      r.error_string(e != ncclSuccess ? e : e2));
@@ -361,7 +434,7 @@ extern "C" int ba_comm_allgather_votes_device(struct ba_comm* comm, uint32_t n, 
 // enqueued, aborts itself (its peers then leave through their watchdog): it
 // never returns as if nothing failed while its peers wait for it.
 static int finish_job(ba_comm* comm, int local_rc, ba_counters* counters_out, bool sum_counters) {
-    if (comm->aborted) return local_rc != BA_OK ? local_rc : fail_aborted(comm);
+    if (comm->aborted.load()) return local_rc != BA_OK ? local_rc : fail_aborted(comm);
     uint64_t* h = comm->h_pin;  // pinned: the copies below never block the host
     if (local_rc != BA_OK) {
         h[BA_NCOUNTERS] = 1;
@@ -372,14 +445,18 @@ static int finish_job(ba_comm* comm, int local_rc, ba_counters* counters_out, bo
         }
     }
     Rccl& r = rccl();
-    const ncclResult_t e = sum_counters
-        ? r.all_reduce(comm->d_cnt, comm->d_cnt, BA_NCOUNTERS, ncclUint64, ncclSum, comm->comm,
-                       comm->stream)
-        : r.all_reduce(comm->d_cnt + kErrSlot, comm->d_cnt + kErrSlot, 1, ncclUint64, ncclSum,
-                       comm->comm, comm->stream);
+    mark_exchange(comm);
+    const ncclResult_t e = with_comm(comm, [&](ncclComm_t cm) {
+        return sum_counters
+            ? r.all_reduce(comm->d_cnt, comm->d_cnt, BA_NCOUNTERS, ncclUint64, ncclSum, cm, comm->stream)
+            : r.all_reduce(comm->d_cnt + kErrSlot, comm->d_cnt + kErrSlot, 1, ncclUint64, ncclSum, cm,
+                           comm->stream);
+    });
     if (e != ncclSuccess) {
+        const bool by_peer = comm->aborted.load();  // ba_comm_abort ran meanwhile
         abort_comm(comm);
         return local_rc != BA_OK ? local_rc
+               : by_peer         ? fail_aborted(comm)
                                  : failf(BA_EDEVICE, "ncclAllReduce: %s (communicator aborted)",
                                          r.error_string(e));
     }
@@ -396,6 +473,12 @@ static int finish_job(ba_comm* comm, int local_rc, ba_counters* counters_out, bo
     if (tmp.v[kErrSlot] != 0)
         return failf(BA_EDEVICE, "%llu other rank(s) failed this call",
                      (unsigned long long)tmp.v[kErrSlot]);
+    // a cascade hand-off poll that ran out of time (ba_cascade.hip): all-reduced
+    // with the counters (trial-DP), so every rank of the job reports it
+    if (tmp.v[BA_C_CHECK_MISMATCH] != 0)
+        return failf(BA_EDEVICE, "in-launch hand-off timed out (%llu stale granule poll(s), counter "
+                     "slot %d); results invalid", (unsigned long long)tmp.v[BA_C_CHECK_MISMATCH],
+                     BA_C_CHECK_MISMATCH);
     tmp.v[kErrSlot] = 0;
     if (counters_out) *counters_out = tmp;
     return BA_OK;
@@ -443,8 +526,11 @@ static int preagree(ba_comm* comm, int local_rc) {
                                              "nor set on the device; communicator aborted");
         }
     }
-    const ncclResult_t e = r.all_reduce(comm->d_cnt + kErrSlot, comm->d_cnt + kErrSlot, 1, ncclUint64,
-                                        ncclSum, comm->comm, comm->stream);
+    mark_exchange(comm);
+    const ncclResult_t e = with_comm(comm, [&](ncclComm_t cm) {
+        return r.all_reduce(comm->d_cnt + kErrSlot, comm->d_cnt + kErrSlot, 1, ncclUint64, ncclSum, cm,
+                            comm->stream);
+    });
     if (e != ncclSuccess) {
         abort_comm(comm);
         return local_rc != BA_OK ? local_rc
@@ -470,7 +556,7 @@ static int preagree(ba_comm* comm, int local_rc) {
 }
 
 static int begin_job(ba_comm* comm) {
-    if (comm->aborted) return fail_aborted(comm);
+    if (comm->aborted.load()) return fail_aborted(comm);
     if (hipSetDevice(comm->device) != hipSuccess || hipMemsetAsync(comm->d_cnt, 0,
             BA_NCOUNTERS * sizeof(uint64_t), comm->stream) != hipSuccess) {
         abort_comm(comm);  // this rank cannot take part: its peers leave through their watchdog

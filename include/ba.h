@@ -120,10 +120,22 @@ typedef struct ba_params {
 #define BA_C_BOUND_VIOL 9      /* in-bound trials violating IC1 or IC2               */
 #define BA_C_FAULTY_TOTAL 10   /* sum of f over trials                               */
 #define BA_C_ATTACK_DECISIONS 11 /* lieutenant decisions == attack                   */
-/* Slot 14 is test-only: hand-off tag mismatches counted by the LEVELS cascade's
- * check build (environment BA_CASC_CHECK=1, read per call; 0 on a correct run),
- * and in every build a granule hand-off that stayed stale past its bounded poll
- * (never on a correct run).
+/* Slot 14 (BA_C_CHECK_MISMATCH = BA_C_HANDOFF_LOST): non-zero means the call's
+ * results are INVALID.  Every build counts there a granule hand-off of the
+ * LEVELS cascade that stayed stale past its bounded poll (2 s; never on a
+ * correct run -- a launch starved by other work on the GPU, or preempted that
+ * long), and the check build (environment BA_CASC_CHECK=1, read per call; a
+ * test switch) also counts hand-off tag mismatches there.  ba_run_trials and
+ * the multi-rank jobs (ba_run_trials_multi, ba_run_instance_split*_multi) read
+ * it back and return BA_EDEVICE ("in-launch hand-off timed out") instead of
+ * results.  Callers of the asynchronous device entries (ba_run_trials_device,
+ * ba_root_from_split_votes_device) MUST check slot 14 of their counters after
+ * synchronizing before trusting decisions, outcomes or counters (ba_amd/lib.py:
+ * check_handoff).  After such an error the ctx stays usable (every eager launch
+ * tags its hand-offs with a new epoch); a captured graph repeats its launch's
+ * epoch, so a graph whose replay reported it must be captured again.
+ * BA_TEST_GRANULE_TICKS (tests only, read per call) shrinks the poll bound
+ * (s_memrealtime ticks, 100 MHz) so a launch times out.
  * The cascade's in-launch hand-offs between workgroups rest on gfx950 / ROCm 7.2
  * behaviour measured in MI355X_MICROARCH.md, not on the HIP memory model:
  * granules ({32-bit value half, 32-bit launch tag} in one aligned 8-byte sc1
@@ -135,6 +147,7 @@ typedef struct ba_params {
  * tests (tests/test_gpu_cascade.py, part of the GPU suite) watch both.
  * Slot 15 is the multi-GPU entries' error flag (always 0 in returned counters). */
 #define BA_C_CHECK_MISMATCH 14
+#define BA_C_HANDOFF_LOST BA_C_CHECK_MISMATCH
 
 typedef struct ba_counters {
     uint64_t v[BA_NCOUNTERS];

@@ -66,6 +66,31 @@ for s in $STAGES; do
     c5) run c5_1024 300 python -u tools/config5_prof.py --batch 1024 --split || exit $?
         run c5_1 300 python -u tools/config5_prof.py --batch 1 --reps 500 --split || exit $? ;;
     multirank) run pytest_multirank 900 python -u -m pytest tests/test_multirank_gpu.py tests/test_dist.py -m gpu -v --timeout 420 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
+    mt) run pytest_mt 300 python -u -m pytest tests/test_gpu_mt.py tests/test_gpu_fullsize.py -m gpu -v -k "mt or table or config1" --timeout 200 --timeout-method thread; rc=$?; fatal $rc && exit $rc
+        run config1 300 python -u tools/run_configs.py --only 1 || exit $? ;;
+    c1) for nn in 4 10; do run config1_n$nn 200 python -u tools/config1_prof.py --n $nn || exit $?; done ;;
+    c1ab) for nn in 4 10; do run config1_r05_n$nn 200 env BA_HIP_LIB=$ROOT/labbuild/mt_r05.so python -u tools/config1_prof.py --n $nn || exit $?
+          run config1_cur_n$nn 200 python -u tools/config1_prof.py --n $nn || exit $?; done ;;
+    c1prof) for nn in 4 10; do
+          (cd /tmp && export TMPDIR=/tmp && mkdir -p "$ROOT/gpurun_out/c1prof_$nn" && \
+           timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/c1prof_$nn" -o run -- \
+             python3 "$ROOT/tools/config1_prof.py" --n $nn > "$ROOT/gpurun_out/c1prof_$nn.log" 2>&1); rc=$?
+          echo "c1prof $nn rc=$rc" | tee -a gpurun_out/steps.log; [ $rc -eq 0 ] || exit $rc; done ;;
+    c1pmc) for nn in 4 10; do
+         C1="$ROOT/tools/config1_prof.py --n $nn --reps 3"
+         for pass in "sq:SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
+                     "lds:SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
+                     "fetch:FETCH_SIZE GRBM_GUI_ACTIVE GRBM_COUNT" "write:WRITE_SIZE"; do
+           name=${pass%%:*}; ctrs=${pass#*:}
+           (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $ctrs --output-format csv \
+              -d "$ROOT/gpurun_out/c1pmc_$nn" -o "$name" -- python3 $C1 > "$ROOT/gpurun_out/c1pmc_${nn}_$name.log" 2>&1)
+           rc=$?; echo "c1pmc $nn $name rc=$rc" | tee -a gpurun_out/steps.log; [ $rc -eq 0 ] || exit $rc
+         done
+         python3 tools/pmc_summary.py gpurun_out/c1pmc_$nn gpurun_out/c1pmc_${nn}_summary.json \
+           --workload "tools/config1_prof.py --n $nn: ba.py-exact OM(1), 1048576 trials" \
+           --config $nn,1,1048576,mt_table,k_mt_table > gpurun_out/c1pmc_${nn}_summary.log 2>&1
+       done ;;
+    handoff) run pytest_handoff 300 python -u -m pytest tests/test_gpu_handoff.py -m gpu -v --timeout 120 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
     casc) run pytest_casc 600 python -u -m pytest tests/test_gpu_cascade.py tests/test_dist.py -m gpu -v --timeout 200 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
     c5prof) for b in 1024 1; do
           (cd /tmp && export TMPDIR=/tmp && mkdir -p "$ROOT/gpurun_out/c5prof_$b" && \
