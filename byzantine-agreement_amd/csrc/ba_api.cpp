@@ -982,7 +982,7 @@ extern "C" int ba_mt_table_device(ba_ctx* ctx, uint32_t n, uint32_t m, uint64_t 
         if (chunk == 0) return fail(BA_ETOOBIG, "scratch budget %zu < %llu B", ctx->scratch_budget,
                                     (unsigned long long)per);
         int rc;
-        if ((rc = ctx->scratch.grow(chunk * per)) != BA_OK) return rc;
+        if ((rc = ctx->scratch.grow(mt_table_state_rows(chunk) * per)) != BA_OK) return rc;
         for (uint64_t c0 = 0; c0 < batch; c0 += chunk) {
             const uint64_t T = batch - c0 < chunk ? batch - c0 : chunk;
             HIP_TRY(launch_mt_table(n, m, T, d_seeds + c0, d_faulty_mask + c0,

@@ -180,6 +180,7 @@ hipError_t launch_table(const RunArgs& a, uint64_t* partials);
 hipError_t launch_gen_inputs(const RunArgs& a, uint32_t* faulty_out, uint8_t* order_out);
 // ba_mtdev.hip: ba.py's coin table on the device (ba_mt_table_device)
 uint64_t mt_table_state_bytes_per_trial();
+uint64_t mt_table_state_rows(uint64_t T);  // row length of the chunk's state: T rounded up to the kernel's blocks
 hipError_t launch_mt_table(uint32_t n, uint32_t m, uint64_t T, const uint64_t* seeds,
                            const uint32_t* faulty, const uint32_t* poll, uint32_t stride,
                            uint32_t* table, uint32_t* next_word, uint32_t* state, hipStream_t s,

@@ -29,6 +29,13 @@ namespace ba {
 namespace {
 
 constexpr int kMtN = 624, kMtM = 397;
+#ifndef BA_MT_BLK
+#define BA_MT_BLK 8
+#endif
+#ifndef BA_MT_TPL
+#define BA_MT_TPL 2
+#endif
+constexpr uint32_t kMtDrawBlk = BA_MT_BLK;  // outputs twisted per block of loads (mt_draw)
 
 struct MtInitTable {
     uint32_t v[kMtN];
@@ -74,7 +81,7 @@ template <typename Slot>
 __device__ __forceinline__ bool mt_draw(uint32_t* __restrict__ st, uint64_t T, uint64_t t, Slot slot,
                                         uint32_t lim, uint32_t cnt, bool want_next, uint32_t* row,
                                         uint32_t* __restrict__ next_word) {
-    constexpr uint32_t kBlk = 16;
+    constexpr uint32_t kBlk = kMtDrawBlk;
     uint32_t pos = 0, c = 0, word = 0;
     bool done = !want_next && cnt == 0, ok = true;
     while (__any(!done)) {
@@ -140,125 +147,182 @@ __device__ __forceinline__ uint32_t mt_mix_step(uint32_t c1, uint32_t c2, uint32
     return (c1 ^ ((c2 ^ (c2 >> 30)) * 1566083941u)) - i;
 }
 
-// Mixing-sweep steps i in [i0, i1) (uniform bounds), the key sweep's mt[i]
-// recomputed alongside; STORE: mt[i] to *p, p advancing one row (T words) per
-// step.  Unrolled so the constant table's scalar loads go out in groups.
-template <bool STORE>
-__device__ __forceinline__ void mt_mix_range(uint32_t i0, uint32_t i1, uint32_t& c1, uint32_t& c2,
-                                             uint32_t add_even, uint32_t add_odd, uint32_t*& p,
-                                             uint64_t T) {
-#pragma unroll 8
+// Mixing-sweep steps i in [i0, i1) (uniform bounds) of J trials at once (J
+// independent recurrence chains per lane: the sweep is a chain of dependent
+// multiplies, so its issue rate is the chains in flight), each with the key
+// sweep's mt[i] recomputed alongside; STORE: mt[i] to *p[j], the pointers
+// advancing one row (R words) per step.  Unrolled so the constant table's
+// scalar loads go out in groups.
+template <int J, bool STORE>
+__device__ __forceinline__ void mt_mix_range(uint32_t i0, uint32_t i1, uint32_t (&c1)[J], uint32_t (&c2)[J],
+                                             const uint32_t (&add_even)[J], const uint32_t (&add_odd)[J],
+                                             uint32_t* (&p)[J], uint64_t R) {
+#pragma unroll 4
     for (uint32_t i = i0; i < i1; ++i) {
-        c1 = mt_key_step(kMtInit.v[i], c1, ((i - 1) & 1) ? add_odd : add_even);
-        c2 = mt_mix_step(c1, c2, i);
-        if constexpr (STORE) {
-            *p = c2;
-            p += T;
-        }
+        const uint32_t init = kMtInit.v[i];
+        const bool odd = ((i - 1) & 1) != 0;
+        static_for<0, J>([&](auto j) {
+            c1[j()] = mt_key_step(init, c1[j()], odd ? add_odd[j()] : add_even[j()]);
+            c2[j()] = mt_mix_step(c1[j()], c2[j()], i);
+            if constexpr (STORE) {
+                *p[j()] = c2[j()];
+                p[j()] += R;
+            }
+        });
     }
 }
 
-// random.seed(seed)'s state (init_by_array, CPython), storing positions
-// [2, lo_end) at rows 2.. and [397, 397 + hi) at rows from lo_end on (rows of
-// T words from st0 = the lane's column), positions 1 and 0 at rows 1 and 0.
-// lo_end = 624, hi = 0: the full state, row = position.  The key sweep is a
-// recurrence over i whose values the mixing sweep needs again, index by index:
-// it is run once to its end (for mt[623] and the wrap step's mt[1]) and once
-// more in lockstep with the mixing sweep, so nothing of it is stored.
-__device__ __forceinline__ void mt_seed(uint32_t* st0, uint64_t T, uint64_t seed, uint32_t lo_end,
-                                        uint32_t hi) {
-    // random.seed(seed): key = the 32-bit limbs of |seed| (one zero limb for 0)
-    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-    const bool two = k1 != 0;
-    // key sweep step at index i adds key[j] + j, j = (i - 1) % len
-    const uint32_t add_even = k0, add_odd = two ? k1 + 1u : k0;
-    // 1. the key sweep to its end: p1 = mt[1] after its first step, a = mt[623]
-    const uint32_t p1 = mt_key_step(kMtInit.v[1], kMtInit.v[0], add_even);
-    uint32_t a = p1;
-#pragma unroll 8
-    for (uint32_t i = 2; i < (uint32_t)kMtN; ++i) a = mt_key_step(kMtInit.v[i], a, ((i - 1) & 1) ? add_odd : add_even);
-    // its 624th step wraps to i = 1 (mt[0] = mt[623], j = 623 % len)
-    const uint32_t p1w = (p1 ^ ((a ^ (a >> 30)) * 1664525u)) + add_odd;
+// random.seed(seed[j])'s state (init_by_array, CPython) for J trials: rows
+// 2..lo_end-1 hold positions 2..lo_end-1 and rows lo_end.. positions 397..
+// 397+hi-1 (rows of R words from col[j] = the trial's column), rows 1 and 0
+// positions 1 and 0 -- every trial of the wave the same rows (whole-wave
+// stores: storing only each trial's own positions, a store of some lanes,
+// measured 1.6x slower at n=10: partial lines).  lo_end = 624, hi = 0: the
+// full state, row = position.  The
+// key sweep is a recurrence over i whose values the mixing sweep needs again,
+// index by index: it is run once to its end (for mt[623] and the wrap step's
+// mt[1]) and once more in lockstep with the mixing sweep, so nothing of it is
+// stored.
+template <int J>
+__device__ __forceinline__ void mt_seed(uint32_t* const (&col)[J], uint64_t R, const uint64_t (&seed)[J],
+                                        uint32_t lo_end, uint32_t hi) {
+    uint32_t add_even[J], add_odd[J], p1[J], a[J];
+    static_for<0, J>([&](auto j) {
+        // random.seed(seed): key = the 32-bit limbs of |seed| (one zero limb for 0);
+        // key sweep step at index i adds key[k] + k, k = (i - 1) % len
+        const uint32_t k0 = (uint32_t)seed[j()], k1 = (uint32_t)(seed[j()] >> 32);
+        add_even[j()] = k0;
+        add_odd[j()] = k1 != 0 ? k1 + 1u : k0;
+        // 1. the key sweep to its end: p1 = mt[1] after its first step, a = mt[623]
+        p1[j()] = mt_key_step(kMtInit.v[1], kMtInit.v[0], add_even[j()]);
+        a[j()] = p1[j()];
+    });
+#pragma unroll 4
+    for (uint32_t i = 2; i < (uint32_t)kMtN; ++i) {
+        const uint32_t init = kMtInit.v[i];
+        const bool odd = ((i - 1) & 1) != 0;
+        static_for<0, J>([&](auto j) { a[j()] = mt_key_step(init, a[j()], odd ? add_odd[j()] : add_even[j()]); });
+    }
+    // its 624th step wraps to i = 1 (mt[0] = mt[623], k = 623 % len)
+    uint32_t c1[J], c2[J], p1w[J];
+    uint32_t* p[J];
+    static_for<0, J>([&](auto j) {
+        p1w[j()] = (p1[j()] ^ ((a[j()] ^ (a[j()] >> 30)) * 1664525u)) + add_odd[j()];
+        c1[j()] = p1[j()];
+        c2[j()] = p1w[j()];
+        p[j()] = col[j()] + 2 * R;
+    });
     // 2. the mixing sweep, i = 2 .. 623; then its wrap step for mt[1], and
     //    mt[0] = 0x80000000
-    uint32_t c1 = p1, c2 = p1w;
-    uint32_t* p = st0 + 2 * T;
     if (hi == 0) {  // the full state
-        mt_mix_range<true>(2u, (uint32_t)kMtN, c1, c2, add_even, add_odd, p, T);
+        mt_mix_range<J, true>(2u, (uint32_t)kMtN, c1, c2, add_even, add_odd, p, R);
     } else {
-        mt_mix_range<true>(2u, lo_end, c1, c2, add_even, add_odd, p, T);
-        mt_mix_range<false>(lo_end, (uint32_t)kMtM, c1, c2, add_even, add_odd, p, T);
-        mt_mix_range<true>((uint32_t)kMtM, (uint32_t)kMtM + hi, c1, c2, add_even, add_odd, p, T);
-        mt_mix_range<false>((uint32_t)kMtM + hi, (uint32_t)kMtN, c1, c2, add_even, add_odd, p, T);
+        mt_mix_range<J, true>(2u, lo_end, c1, c2, add_even, add_odd, p, R);
+        mt_mix_range<J, false>(lo_end, (uint32_t)kMtM, c1, c2, add_even, add_odd, p, R);
+        mt_mix_range<J, true>((uint32_t)kMtM, (uint32_t)kMtM + hi, c1, c2, add_even, add_odd, p, R);
+        mt_mix_range<J, false>((uint32_t)kMtM + hi, (uint32_t)kMtN, c1, c2, add_even, add_odd, p, R);
     }
-    st0[T] = (p1w ^ ((c2 ^ (c2 >> 30)) * 1566083941u)) - 1u;
-    st0[0] = 0x80000000u;
+    static_for<0, J>([&](auto j) {
+        col[j()][R] = (p1w[j()] ^ ((c2[j()] ^ (c2[j()] >> 30)) * 1566083941u)) - 1u;
+        col[j()][0] = 0x80000000u;
+    });
 }
 
-// One thread per trial.  The state goes to HBM [slot][T] (every step of a wave
-// one coalesced 256-B access), but only the positions the round's outputs read
-// (round 6: the whole 624-word state was written, 2.5 KB per trial, and the
-// kernel was bound by those writes): a round of D <= 227 outputs reads
-// positions 0..D and 397..397+D-1, and a few more past 227 (the in-place twist
-// reads its own new words there).  Each wave sizes its window from its lanes'
-// coin counts (om1_coins): Wv = max over the wave of 2.5 cnt + 16 (+1 for the
-// next word; a coin takes 2 outputs on average, so that is > 4 sigma of
-// retries), rounded to the draw block.  A lane that still needs more outputs
-// starts over on its full 624-word state (positions = slots), as does every
-// lane of a wave whose window would not fit in 624 slots.
-__global__ __launch_bounds__(256) void k_mt_table(uint32_t n, uint32_t m, uint64_t T,
-                                                  const uint64_t* __restrict__ seeds,
-                                                  const uint32_t* __restrict__ faulty,
-                                                  const uint32_t* __restrict__ poll, uint32_t stride,
-                                                  uint32_t* __restrict__ table,
-                                                  uint32_t* __restrict__ next_word,
-                                                  uint32_t* __restrict__ st) {
-    constexpr uint32_t kBlk = 16, kFar = kMtN - kMtM;  // 227 outputs before a wrap
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool live = t < T;
+// kMtTrialsPerLane trials per thread, the block's 256 threads owning 512
+// consecutive trials: trial t_j = block * 512 + j * 256 + thread, so every
+// store of a wave is one coalesced 256-B row segment.  The state goes to HBM
+// [slot][R] (R = the chunk rounded up to whole blocks: a block's trials past
+// the chunk's end run on zero inputs into padding columns, branch-free), but
+// only the positions the round's outputs read (round 6: the whole 624-word
+// state was written, 2.5 KB per trial, and the kernel was bound by those
+// writes): a round of D <= 227 outputs reads positions 0..D and 397..397+D-1,
+// and a few more past 227 (the in-place twist reads its own new words there).
+// Each wave sizes its window from its trials' coin counts (om1_coins): Wv = max
+// over the wave of 2.5 cnt + 16 (+1 for the next word; a coin takes 2 outputs
+// on average, so that is > 4 sigma of retries), rounded to the draw block.  A
+// trial that still needs more outputs starts over on its full 624-word state
+// (positions = slots), as does every trial of a wave whose window would not
+// fit below position 397.
+constexpr int kMtTrialsPerLane = BA_MT_TPL, kMtBlock = 256;
+
+__global__ __launch_bounds__(kMtBlock) void k_mt_table(uint32_t n, uint32_t m, uint64_t T, uint64_t R,
+                                                       const uint64_t* __restrict__ seeds,
+                                                       const uint32_t* __restrict__ faulty,
+                                                       const uint32_t* __restrict__ poll, uint32_t stride,
+                                                       uint32_t* __restrict__ table,
+                                                       uint32_t* __restrict__ next_word,
+                                                       uint32_t* __restrict__ st) {
+    constexpr int J = kMtTrialsPerLane;
+    constexpr uint32_t kBlk = kMtDrawBlk, kFar = kMtN - kMtM;  // 227 outputs before a wrap
     const bool want_next = next_word != nullptr;
-    const uint32_t cnt = live ? om1_coins(n, m, faulty[t], poll ? poll[t] : 0u) : 0u;
-    uint32_t need = (!live || (cnt == 0 && !want_next)) ? 0u : 2u * cnt + cnt / 2u + 16u + (want_next ? 1u : 0u);
+    uint64_t t[J], seed[J];
+    uint32_t cnt[J], need = 0;
+    bool live[J];
+    uint32_t* col[J];
+    static_for<0, J>([&](auto j) {
+        t[j()] = (uint64_t)blockIdx.x * (kMtBlock * J) + j() * kMtBlock + threadIdx.x;
+        live[j()] = t[j()] < T;
+        cnt[j()] = live[j()] ? om1_coins(n, m, faulty[t[j()]], poll ? poll[t[j()]] : 0u) : 0u;
+        seed[j()] = live[j()] ? seeds[t[j()]] : 0ull;
+        col[j()] = st + t[j()];  // t < R: padding columns for the dead trials
+        // the outputs this trial's window holds (whole draw blocks)
+        const uint32_t nj = live[j()] && (cnt[j()] != 0 || want_next)
+                                ? 2u * cnt[j()] + cnt[j()] / 2u + 16u + (want_next ? 1u : 0u) : 0u;
+        need = max(need, (nj + kBlk - 1) / kBlk * kBlk);
+    });
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) need = max(need, (uint32_t)__shfl_xor((int)need, off, 64));
-    if (!live) return;
     // the wave-uniform window (outputs)
-    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)((need + kBlk - 1) / kBlk * kBlk));
-    uint32_t* row = table + t * stride;
-    const uint64_t seed = seeds[t];
-    uint32_t* col = st + t;
-    bool ok = true;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)need);
+    bool ok[J];
+    static_for<0, J>([&](auto j) { ok[j()] = true; });
     if (wv == 0) {
-        // no lane of the wave draws: random.seed's state is never read
+        // no trial of the wave draws: random.seed's state is never read
     } else if (wv < (uint32_t)kMtM) {
         // window: positions 0..wv at rows 0..wv, 397..397+min(wv,227)-1 after them
-        // (below 624 rows; outputs past 227 read positions <= wv back as new)
+        // (outputs past 227 read positions <= wv back as new)
         const uint32_t hi = wv < kFar ? wv : kFar;
-        mt_seed(col, T, seed, wv + 1, hi);
+        mt_seed<J>(col, R, seed, wv + 1, hi);
         auto slot = [wv](uint32_t i) { return i <= wv ? i : wv + 1u + (i - (uint32_t)kMtM); };
-        ok = mt_draw(st, T, t, slot, wv, cnt, want_next, row, next_word);
+        static_for<0, J>([&](auto j) {
+            if (live[j()])
+                ok[j()] = mt_draw(st, R, t[j()], slot, wv, cnt[j()], want_next, table + t[j()] * stride,
+                                  next_word);
+        });
     } else {
-        ok = false;
+        static_for<0, J>([&](auto j) { ok[j()] = false; });
     }
-    if (!ok) {  // the full state: every position at its own row, any number of outputs
-        mt_seed(col, T, seed, (uint32_t)kMtN, 0u);
-        (void)mt_draw(st, T, t, [](uint32_t i) { return i; }, 0u, cnt, want_next, row, next_word);
-    }
-    for (uint32_t wi = (cnt + 31) >> 5; wi < stride; ++wi) row[wi] = 0;  // the row's unused words
+    static_for<0, J>([&](auto j) {
+        if (!live[j()]) return;
+        uint32_t* row = table + t[j()] * stride;
+        if (!ok[j()]) {  // the full state: every position at its own row, any number of outputs
+            uint32_t* const c1[1] = {col[j()]};
+            const uint64_t s1[1] = {seed[j()]};
+            mt_seed<1>(c1, R, s1, (uint32_t)kMtN, 0u);
+            (void)mt_draw(st, R, t[j()], [](uint32_t i) { return i; }, 0u, cnt[j()], want_next, row, next_word);
+        }
+        for (uint32_t wi = (cnt[j()] + 31) >> 5; wi < stride; ++wi) row[wi] = 0;  // the row's unused words
+    });
 }
 
 }  // namespace
 
-// state words per trial (the chunk's scratch: [624][T] uint32)
+// the chunk's scratch: [624][R] uint32, R = the chunk's trials rounded up to
+// whole blocks of kMtTrialsPerLane * kMtBlock
 uint64_t mt_table_state_bytes_per_trial() { return (uint64_t)kMtN * sizeof(uint32_t); }
+uint64_t mt_table_state_rows(uint64_t T) {
+    constexpr uint64_t b = (uint64_t)kMtTrialsPerLane * kMtBlock;
+    return (T + b - 1) / b * b;
+}
 
 hipError_t launch_mt_table(uint32_t n, uint32_t m, uint64_t T, const uint64_t* seeds,
                            const uint32_t* faulty, const uint32_t* poll, uint32_t stride,
                            uint32_t* table, uint32_t* next_word, uint32_t* state, hipStream_t s,
                            Prof* prof) {
     ProfScope ps(prof, "k_mt_table", s);
-    const uint64_t blocks = (T + 255) / 256;
-    hipLaunchKernelGGL(k_mt_table, dim3((uint32_t)blocks), dim3(256), 0, s, n, m, T, seeds, faulty,
+    const uint64_t R = mt_table_state_rows(T);
+    const uint64_t blocks = R / ((uint64_t)kMtTrialsPerLane * kMtBlock);
+    hipLaunchKernelGGL(k_mt_table, dim3((uint32_t)blocks), dim3(kMtBlock), 0, s, n, m, T, R, seeds, faulty,
                        poll, stride, table, next_word, state);
     return hipGetLastError();
 }

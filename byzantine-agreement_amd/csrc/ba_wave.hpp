@@ -569,9 +569,18 @@ __device__ __forceinline__ void opaque_v(uint64_t& x) { asm volatile("" : "+v"(x
 //   mem[a] = 8 (a + (a >= la)): member a's word in the E row (below)
 //   r2t[d] = 8 (C + 1) (d >= la): member d's R2T row is d + (d >= la); the
 //            8 (C + 1) d part is the store's immediate offset
+// LDS row paddings of k_om3w (lab A/B only: tools/lds_bank_model.py predicts
+// each group's bank conflicts; BA_OM3W_R2T_PAD = 1 keeps the R2T column reads
+// conflict-free, BA_OM3W_R1T_PAD = 0 the R1T rows unpadded)
+#ifndef BA_OM3W_R2T_PAD
+#define BA_OM3W_R2T_PAD 1
+#endif
+#ifndef BA_OM3W_R1T_PAD
+#define BA_OM3W_R1T_PAD 0
+#endif
 template <int N>
 struct Om3LaneOffsets {
-    static constexpr int S = N - 3, CP = N - 1;
+    static constexpr int S = N - 3, CP = N - 2 + BA_OM3W_R2T_PAD;
     LaneBytes<S> mem, r2t;
     __device__ __forceinline__ explicit Om3LaneOffsets(uint32_t la)
         : mem([la](int a) { return 8u * (a + ((uint32_t)a >= la ? 1u : 0u)); }),
@@ -600,7 +609,7 @@ __device__ __forceinline__ uint64_t om3_round(const uint64_t* in, uint64_t l0j1,
                                               uint64_t seed, uint64_t gw,
                                               uint64_t* erow = nullptr,
                                               const Om3LaneOffsets<N>* lo_ = nullptr) {
-    constexpr int L = N - 1, S = N - 3, C = L - 1, CP = C + 1;
+    constexpr int L = N - 1, S = N - 3, C = L - 1, CP = C + BA_OM3W_R2T_PAD;
     constexpr uint32_t ME = 3;
     const uint32_t sr = j1 * C + la;             // level-1 slot (j1, j2)
     const uint32_t j2 = la + (la >= j1);
@@ -729,11 +738,12 @@ struct Om3W {
     static constexpr int BPC = 2;                  // launch cap: blocks per CU
     static constexpr int LANES = W * C;            // lanes busy in the subtree rounds
     static constexpr int NIN = N + 3;
-    static constexpr int CP = C + 1;               // padded R2T row (om3_round)
-    // IN[W][NIN] | L0[W][L] | R2T[W][C][CP] | R1T[W][L][L] (root inputs, receiver-major:
+    static constexpr int CP = C + BA_OM3W_R2T_PAD;  // padded R2T row (om3_round)
+    static constexpr int LP = L + BA_OM3W_R1T_PAD;  // R1T row
+    // IN[W][NIN] | L0[W][L] | R2T[W][C][CP] | R1T[W][L][LP] (root inputs, receiver-major:
     // R1T[w][j2][j1] = R1[j1, j2], L0[j2] on the diagonal) ; A/U roots reuse R2T
     static constexpr int oIN = 0, oL0 = oIN + W * NIN, oR2 = oL0 + W * L, oR1 = oR2 + W * C * CP;
-    static constexpr int oE = oR1 + W * L * L;     // E[W][C + 1] (om3_round EROW mode)
+    static constexpr int oE = oR1 + W * L * LP;    // E[W][C + 1] (om3_round EROW mode)
     static constexpr int end0 = oE + W * (C + 1);
     static constexpr bool au_in_r2 = 2 * L <= C * CP;
     static constexpr int oAU = au_in_r2 ? oR2 : end0;
@@ -742,7 +752,7 @@ struct Om3W {
 
 // Level 0 of a task's W words (one Philox per slot pair) into l0[w*L + j] and
 // the diagonal r1t[(w*L + j)*L + j] (root column j counts L0[j] as its own input).
-template <int N, int W>
+template <int N, int W, int LP = N - 1>
 __device__ __forceinline__ void level0_r1t(const uint64_t* in0, uint64_t* l0, uint64_t* r1t,
                                            uint32_t lane, uint64_t seed, uint64_t gw0) {
     constexpr int L = N - 1, NIN = N + 3;
@@ -758,7 +768,7 @@ __device__ __forceinline__ void level0_r1t(const uint64_t* in0, uint64_t* l0, ui
             if (j < (uint32_t)L) {
                 const uint64_t v = (F0 & lv[h()]) | (~F0 & ob);
                 l0[w * L + j] = v;
-                r1t[(w * L + j) * L + j] = v;
+                r1t[(w * L + j) * LP + j] = v;
             }
         });
     }
@@ -768,11 +778,11 @@ __device__ __forceinline__ void level0_r1t(const uint64_t* in0, uint64_t* l0, ui
 // compile-time carry-save count): strict majority attacks, a tie is
 // "undefined" (ba.py:188-195; only an even L ties).  au[w*2L + b] = A,
 // au[w*2L + L + b] = U.
-template <int L, int W>
+template <int L, int W, int LP = L>
 __device__ __forceinline__ void roots_r1t(const uint64_t* r1t0, uint64_t* au, uint32_t lane) {
     for (uint32_t it = lane; it < (uint32_t)W * L; it += 64) {
         const uint32_t w = it / L, col = it - w * L;
-        const uint64_t* r1t = r1t0 + (w * L + col) * L;
+        const uint64_t* r1t = r1t0 + (w * L + col) * LP;
         Csa<planes_c(L)> cnt;
         static_for<0, L>([&](auto j) { cnt.template add<j()>(r1t[j()]); });
         const uint64_t att = cnt.template ge<L, L / 2 + 1>();
@@ -867,7 +877,7 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM3W_MIN_BLOCKS(N)) void k_om3w(
             wave_inputs<N, W, DIAG>(img + G::oIN, lane, w0, seed, gs, first_trial, batch, faulty, order);
         __builtin_amdgcn_wave_barrier();
         FUSED_STAMP(0);
-        level0_r1t<N, W>(img + G::oIN, img + G::oL0, img + G::oR1, lane, seed, gw0);
+        level0_r1t<N, W, G::LP>(img + G::oIN, img + G::oL0, img + G::oR1, lane, seed, gw0);
         // E row of round 0: lieutenants 1 .. L-1 (general g's word is in[g])
         const uint64_t* in = img + G::oIN + lw * NIN;
         uint64_t* erow = img + G::oE + lw * (C + 1);
@@ -884,11 +894,11 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM3W_MIN_BLOCKS(N)) void k_om3w(
                                                    erow, &lofs);
             FUSED_STAMP(1);
             // R1[j1, b] is root input j1 of receiver column j2(b)
-            if (act) img[G::oR1 + (lw * L + la + (la >= j1 ? 1u : 0u)) * L + j1] = r1;
+            if (act) img[G::oR1 + (lw * L + la + (la >= j1 ? 1u : 0u)) * G::LP + j1] = r1;
             FUSED_STAMP(2);
         }
         __builtin_amdgcn_wave_barrier();
-        roots_r1t<L, W>(img + G::oR1, img + G::oAU, lane);
+        roots_r1t<L, W, G::LP>(img + G::oR1, img + G::oAU, lane);
         __builtin_amdgcn_wave_barrier();
         FUSED_STAMP(3);
         {

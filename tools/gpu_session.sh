@@ -90,6 +90,22 @@ for s in $STAGES; do
            --workload "tools/config1_prof.py --n $nn: ba.py-exact OM(1), 1048576 trials" \
            --config $nn,1,1048576,mt_table,k_mt_table > gpurun_out/c1pmc_${nn}_summary.log 2>&1
        done ;;
+    c1var) for lib in $C1LIBS; do
+             run mttest_$(basename $lib .so) 200 env BA_HIP_LIB=$ROOT/$lib python -u -m pytest tests/test_gpu_mt.py -m gpu -q --timeout 100 --timeout-method thread || exit $?
+           done
+           for rep in 1 2; do for nn in 4 10; do for lib in $C1LIBS; do
+             echo "lib=$lib n=$nn rep=$rep $(BA_HIP_LIB=$ROOT/$lib timeout -k 10 120 python tools/config1_prof.py --n $nn 2>/dev/null | grep '^{')" >> gpurun_out/c1var.log || exit $?
+           done; done; done ;;
+    bank) for lib in $BANKLIBS; do
+            nm=$(basename $lib .so)
+            (cd /tmp && export TMPDIR=/tmp BA_HIP_LIB=$ROOT/$lib && timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE --output-format csv \
+               -d "$ROOT/gpurun_out/bank_$nm" -o pmc -- python3 $BENCH_PMC > "$ROOT/gpurun_out/bank_$nm.log" 2>&1); rc=$?
+            echo "bank $nm rc=$rc" | tee -a gpurun_out/steps.log; [ $rc -eq 0 ] || exit $rc
+            python3 tools/pmc_summary.py gpurun_out/bank_$nm gpurun_out/bank_${nm}_summary.json --workload "bench.py --streams 1 with $lib" > /dev/null 2>&1
+          done
+          for rep in 1 2; do for lib in $BANKLIBS; do
+            echo "lib=$lib rep=$rep $(BA_HIP_LIB=$ROOT/$lib timeout -k 10 120 python bench.py --steps 20 --warmup 3 --no-cpu --no-profile 2>/dev/null | grep '^{')" >> gpurun_out/bank_bench.log || exit $?
+          done; done ;;
     handoff) run pytest_handoff 300 python -u -m pytest tests/test_gpu_handoff.py -m gpu -v --timeout 120 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
     casc) run pytest_casc 600 python -u -m pytest tests/test_gpu_cascade.py tests/test_dist.py -m gpu -v --timeout 200 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
     c5prof) for b in 1024 1; do
