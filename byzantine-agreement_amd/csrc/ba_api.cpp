@@ -675,6 +675,10 @@ static bool co_admit(ba_ctx* ctx, hipStream_t s, uint64_t pollers) {
     if (stream_capturing(s)) return true;
     std::lock_guard<std::mutex> lk(co_registry().mu);
     uint64_t busy = 0;
+    for (ba_ctx* c : co_registry().ctxs)  // fast path: everything counted as running fits
+        if (c != ctx && c->device == ctx->device) busy += c->co_pending;
+    if (busy + pollers <= budget) return true;
+    busy = 0;
     for (ba_ctx* c : co_registry().ctxs) {
         if (c == ctx || c->device != ctx->device || c->co_pending == 0) continue;
         // a stream being captured may not be queried: its launches count

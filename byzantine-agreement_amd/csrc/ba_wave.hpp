@@ -578,6 +578,14 @@ __device__ __forceinline__ void opaque_v(uint64_t& x) { asm volatile("" : "+v"(x
 #ifndef BA_OM3W_R1T_PAD
 #define BA_OM3W_R1T_PAD 0
 #endif
+// lab ablations for the bank-conflict attribution (results wrong; never built
+// into the product): drop the R2T leaf stores or the R1T store of a round
+#ifndef BA_OM3W_LAB_NO_R2T
+#define BA_OM3W_LAB_NO_R2T 0
+#endif
+#ifndef BA_OM3W_LAB_NO_R1T
+#define BA_OM3W_LAB_NO_R1T 0
+#endif
 template <int N>
 struct Om3LaneOffsets {
     static constexpr int S = N - 3, CP = N - 2 + BA_OM3W_R2T_PAD;
@@ -698,12 +706,16 @@ __device__ __forceinline__ uint64_t om3_round(const uint64_t* in, uint64_t l0j1,
         uint64_t* r2t = r2t_w + lw * C * CP + la;
         char* rb = (char*)r2t;
         leaf_block_emit<S>(ME, seed, gw, sr, diag, Fm, [&](auto d, uint64_t v) {
-            if constexpr (EROW)
+            if constexpr (BA_OM3W_LAB_NO_R2T) {  // lab ablation (wrong results): PMC attribution only
+                asm volatile("" ::"v"(v));
+            } else if constexpr (EROW) {
                 *(uint64_t*)(rb + ofs.r2t.template get<d()>() + 8 * CP * d()) = v;
-            else
+            } else {
                 r2t[(d() + (d() >= la ? 1u : 0u)) * CP] = v;
+            }
         });
-        r2t[la * CP] = par;
+        if constexpr (!BA_OM3W_LAB_NO_R2T) r2t[la * CP] = par;
+        else asm volatile("" ::"v"(par));
     }
     __builtin_amdgcn_wave_barrier();
     uint64_t r1 = 0;
@@ -894,7 +906,8 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM3W_MIN_BLOCKS(N)) void k_om3w(
                                                    erow, &lofs);
             FUSED_STAMP(1);
             // R1[j1, b] is root input j1 of receiver column j2(b)
-            if (act) img[G::oR1 + (lw * L + la + (la >= j1 ? 1u : 0u)) * G::LP + j1] = r1;
+            if constexpr (BA_OM3W_LAB_NO_R1T) asm volatile("" ::"v"(r1));  // lab ablation (wrong results)
+            else if (act) img[G::oR1 + (lw * L + la + (la >= j1 ? 1u : 0u)) * G::LP + j1] = r1;
             FUSED_STAMP(2);
         }
         __builtin_amdgcn_wave_barrier();
@@ -949,6 +962,23 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM3W_MIN_BLOCKS(N)) void k_om3w(
 #ifndef BA_OM4W_BLOCKS_PER_CU
 #define BA_OM4W_BLOCKS_PER_CU 3
 #endif
+// BA_OM4W_PAIRS = 1 (round 6): a round's Philox group drops from S/2 + 3 calls
+// per lane to (S+1)/2.  (a) The level-1 lie words of a j1's C1 rounds come from
+// ONE call per lane per j1 (W x NP1 pairs over the wave's lanes, into L1W in
+// LDS), where every lane drew its round's level-1 pair.  (b) For odd S and even
+// C2 (n = 7, 9, 11, 13) lanes 2k, 2k+1 hold blocks x2 even / odd of one word:
+// they share the level-2 pair x2 >> 1 and the level-3 pair that straddles their
+// blocks, so the even lane draws its five level-3 pairs (the straddling one
+// last), the odd lane its four others and the level-2 pair, and each takes the
+// missing one from its partner with a DPP swap -- and the diagonal lie words
+// become one select per half between the two lanes' layouts, where the odd
+// block's half-pair offset cost three ops per half.  0 = the round-5 group
+// (lab A/B only).
+#ifndef BA_OM4W_PAIRS
+#define BA_OM4W_PAIRS 3  // bit 0: (a), bit 1: (b)
+#endif
+#define BA_OM4W_L1W ((BA_OM4W_PAIRS & 1) != 0)
+#define BA_OM4W_XCH ((BA_OM4W_PAIRS & 2) != 0)
 template <int N>
 struct Om4W {
     static constexpr int L = N - 1, S = N - 4, C1 = L - 1, C2 = L - 2;
@@ -960,7 +990,10 @@ struct Om4W {
     static constexpr int oIN = 0, oL0 = oIN + W * NIN, oR3 = oL0 + W * L;
     static constexpr int oR1 = oR3 + W * C2 * C2, oRC = oR1 + W * C1 * P1;
     static constexpr int oE = oRC + W * L * P;   // E2[W][C2 + 1] (members, see k_om4w)
-    static constexpr int end0 = oE + W * (C2 + 1);
+    // L1W[W][C1]: the level-1 lie words of the current j1's C1 rounds (BA_OM4W_PAIRS)
+    static constexpr int NP1 = C1 / 2 + 1;       // Philox pairs that cover C1 slots
+    static constexpr int oL1 = oE + W * (C2 + 1);
+    static constexpr int end0 = oL1 + (BA_OM4W_L1W ? W * C1 : 0);
     static constexpr bool au_in_r3 = 2 * L <= C2 * C2;
     static constexpr int oAU = au_in_r3 ? oR3 : end0;
     static constexpr int words = ((au_in_r3 ? end0 : end0 + W * 2 * L) + 1) & ~1;
@@ -1030,6 +1063,23 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM4W_BLOCKS_PER_CU) void k_om4w(
             __builtin_amdgcn_wave_barrier();
             const uint64_t fj1 = in[j1 + 1];
             const uint64_t l0j1 = img[G::oL0 + lw * L + j1];
+            if constexpr (BA_OM4W_L1W) {
+                // L1W[w][c2] = the lie word of level-1 slot j1*C1 + c2 of word w:
+                // lane (w, i) draws pair (j1*C1 >> 1) + i and keeps its in-range halves
+                static_assert(W * G::NP1 <= 64, "one L1 pair per lane");
+                const uint32_t s0 = j1 * C1;
+                if (lane < (uint32_t)(W * G::NP1)) {
+                    const uint32_t w = lane / G::NP1, i = lane - w * G::NP1, pr = (s0 >> 1) + i;
+                    const uint64_t g1 = gw0 + w;
+                    P4 q[1] = {P4{pr, 1u, (uint32_t)g1, (uint32_t)(g1 >> 32)}};
+                    philox_groups<1>(q, (uint32_t)seed, (uint32_t)(seed >> 32));  // the rounds' code shape
+                    const uint64_t h0 = (uint64_t)q[0].y << 32 | q[0].x, h1 = (uint64_t)q[0].w << 32 | q[0].z;
+                    const uint32_t c0 = 2 * pr - s0;  // c2 of the pair's first half (may be -1)
+                    if (c0 < (uint32_t)C1) img[G::oL1 + w * C1 + c0] = h0;
+                    if (c0 + 1 < (uint32_t)C1) img[G::oL1 + w * C1 + c0 + 1] = h1;
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
             for (uint32_t c2 = 0; c2 < (uint32_t)C1; ++c2, ++round) {
                 // unlike k_om3w, the per-round priority alternation pays here
                 // (config 3 A/B, round 2: without it 2.8% slower; R3T rows padded
@@ -1051,38 +1101,73 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM4W_BLOCKS_PER_CU) void k_om4w(
                 if (act) {
                     const uint32_t x3 = x2 * S;
                     constexpr int NPD = (S + 1) / 2;
-                    P4 pc[NPD + 2];
-                    static_for<0, NPD>([&](auto qd) {
-                        pc[qd()] = P4{(x3 >> 1) + qd(), 3u, (uint32_t)gw, (uint32_t)(gw >> 32)};
-                    });
-                    pc[NPD] = P4{x2 >> 1, 2u, (uint32_t)gw, (uint32_t)(gw >> 32)};
-                    pc[NPD + 1] = P4{x1 >> 1, 1u, (uint32_t)gw, (uint32_t)(gw >> 32)};
-                    // at most 4 calls in flight (philox10_n's one-statement rounds;
-                    // 7 interleaved calls held ~70 VGPRs at once)
-                    philox_groups<NPD + 2>(pc, (uint32_t)seed, (uint32_t)(seed >> 32));
-                    uint64_t lw3[2 * NPD];
-                    static_for<0, NPD>([&](auto qd) {
-                        lw3[2 * qd()] = (uint64_t)pc[qd()].y << 32 | pc[qd()].x;
-                        lw3[2 * qd() + 1] = (uint64_t)pc[qd()].w << 32 | pc[qd()].z;
-                    });
-                    const uint64_t lie2 = (x2 & 1u) ? ((uint64_t)pc[NPD].w << 32 | pc[NPD].z)
-                                                    : ((uint64_t)pc[NPD].y << 32 | pc[NPD].x);
-                    const uint64_t lie1 = (x1 & 1u) ? ((uint64_t)pc[NPD + 1].w << 32 | pc[NPD + 1].z)
-                                                    : ((uint64_t)pc[NPD + 1].y << 32 | pc[NPD + 1].x);
+                    auto lo = [](const P4& q) { return (uint64_t)q.y << 32 | q.x; };
+                    auto hi = [](const P4& q) { return (uint64_t)q.w << 32 | q.z; };
+                    uint64_t lie3[S], lie2, lie1;
+                    if constexpr (BA_OM4W_XCH && S % 2 == 1 && C2 % 2 == 0) {
+                        // (b): x2 & 1 == la & 1; the odd lane's x3 >> 1 is the
+                        // straddling pair, its own pairs follow it
+                        const bool odd = (la & 1u) != 0;
+                        P4 pc[NPD];
+                        static_for<0, NPD - 1>([&](auto qd) {
+                            pc[qd()] = P4{(x3 >> 1) + qd() + (odd ? 1u : 0u), 3u, (uint32_t)gw,
+                                          (uint32_t)(gw >> 32)};
+                        });
+                        pc[NPD - 1] = odd ? P4{x2 >> 1, 2u, (uint32_t)gw, (uint32_t)(gw >> 32)}
+                                          : P4{(x3 >> 1) + NPD - 1, 3u, (uint32_t)gw, (uint32_t)(gw >> 32)};
+                        philox_groups<NPD>(pc, (uint32_t)seed, (uint32_t)(seed >> 32));
+                        // the half the partner needs of this lane's last call: the even
+                        // lane's straddling pair's second half (the odd block's first
+                        // slot), the odd lane's level-2 pair's first half (x2 even)
+                        const P4& l4 = pc[NPD - 1];
+                        const uint32_t s0x = odd ? l4.x : l4.z, s0y = odd ? l4.y : l4.w;
+                        const uint64_t rcv = (uint64_t)swap_pair(s0y) << 32 | swap_pair(s0x);
+                        // slot x3 + d: even lane half d&1 of pair d>>1; odd lane d = 0 the
+                        // straddling pair's second half, else half (d-1)&1 of pair (d-1)>>1
+                        static_for<0, S>([&](auto d) {
+                            constexpr int e = d();
+                            const uint64_t ev = (e & 1) ? hi(pc[e >> 1]) : lo(pc[e >> 1]);
+                            uint64_t ov;
+                            if constexpr (e == 0) ov = rcv;
+                            else ov = ((e - 1) & 1) ? hi(pc[(e - 1) >> 1]) : lo(pc[(e - 1) >> 1]);
+                            lie3[e] = odd ? ov : ev;
+                        });
+                        lie2 = odd ? hi(l4) : rcv;
+                    } else {
+                        constexpr int NG = NPD + (BA_OM4W_L1W ? 1 : 2);
+                        P4 pc[NG];
+                        static_for<0, NPD>([&](auto qd) {
+                            pc[qd()] = P4{(x3 >> 1) + qd(), 3u, (uint32_t)gw, (uint32_t)(gw >> 32)};
+                        });
+                        pc[NPD] = P4{x2 >> 1, 2u, (uint32_t)gw, (uint32_t)(gw >> 32)};
+                        if constexpr (!BA_OM4W_L1W) pc[NG - 1] = P4{x1 >> 1, 1u, (uint32_t)gw, (uint32_t)(gw >> 32)};
+                        // at most 4 calls in flight (philox10_n's one-statement rounds;
+                        // 7 interleaved calls held ~70 VGPRs at once)
+                        philox_groups<NG>(pc, (uint32_t)seed, (uint32_t)(seed >> 32));
+                        uint64_t lw3[2 * NPD];
+                        static_for<0, NPD>([&](auto qd) {
+                            lw3[2 * qd()] = lo(pc[qd()]);
+                            lw3[2 * qd() + 1] = hi(pc[qd()]);
+                        });
+                        const uint64_t oddmask = 0ull - (uint64_t)(x3 & 1u);
+                        static_for<0, S>([&](auto d) {
+                            if constexpr (S % 2 == 1) lie3[d()] = lw3[d()] ^ ((lw3[d()] ^ lw3[d() + 1]) & oddmask);
+                            else lie3[d()] = lw3[d()];
+                        });
+                        lie2 = (x2 & 1u) ? hi(pc[NPD]) : lo(pc[NPD]);
+                        if constexpr (!BA_OM4W_L1W) lie1 = (x1 & 1u) ? hi(pc[NG - 1]) : lo(pc[NG - 1]);
+                    }
+                    if constexpr (BA_OM4W_L1W) lie1 = img[G::oL1 + lw * C1 + c2];  // (a)
                     l1v = (fj1 & lie1) | (~fj1 & l0j1);              // L1[j1, j2], sender j1
                     const uint64_t fj2 = in[j2 + 1];
                     par = (fj2 & lie2) | (~fj2 & l1v);               // L2[j1, j2, j3], sender j2
                     // members of leaf block (j1, j2, j3): the lieutenants not in
                     // {j1, j2, j3}, ascending = E2 without its entry la
                     const uint64_t fs = erow[la];  // level-3 sender: j3
-                    const uint64_t oddmask = 0ull - (uint64_t)(x3 & 1u);
                     const char* eb = (const char*)erow;
                     uint64_t diag[S], Fm[S];
                     static_for<0, S>([&](auto d) {
-                        uint64_t lie3;
-                        if constexpr (S % 2 == 1) lie3 = lw3[d()] ^ ((lw3[d()] ^ lw3[d() + 1]) & oddmask);
-                        else lie3 = lw3[d()];
-                        diag[d()] = (fs & lie3) | (~fs & par);
+                        diag[d()] = (fs & lie3[d()]) | (~fs & par);
                         Fm[d()] = *(const uint64_t*)(eb + memr.template get<d()>());
                     });
                     uint64_t* r3t = img + G::oR3 + lw * C2 * C2 + la;

@@ -99,13 +99,19 @@ for s in $STAGES; do
     bank) for lib in $BANKLIBS; do
             nm=$(basename $lib .so)
             (cd /tmp && export TMPDIR=/tmp BA_HIP_LIB=$ROOT/$lib && timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE --output-format csv \
-               -d "$ROOT/gpurun_out/bank_$nm" -o pmc -- python3 $BENCH_PMC > "$ROOT/gpurun_out/bank_$nm.log" 2>&1); rc=$?
+               -d "$ROOT/gpurun_out/bank_$nm" -o pmc -- python3 $ROOT/tools/om3w_launch.py > "$ROOT/gpurun_out/bank_$nm.log" 2>&1); rc=$?
             echo "bank $nm rc=$rc" | tee -a gpurun_out/steps.log; [ $rc -eq 0 ] || exit $rc
             python3 tools/pmc_summary.py gpurun_out/bank_$nm gpurun_out/bank_${nm}_summary.json --workload "bench.py --streams 1 with $lib" > /dev/null 2>&1
           done
-          for rep in 1 2; do for lib in $BANKLIBS; do
+          [ -n "${BANKBENCH:-}" ] && for rep in 1 2; do for lib in $BANKLIBS; do
             echo "lib=$lib rep=$rep $(BA_HIP_LIB=$ROOT/$lib timeout -k 10 120 python bench.py --steps 20 --warmup 3 --no-cpu --no-profile 2>/dev/null | grep '^{')" >> gpurun_out/bank_bench.log || exit $?
-          done; done ;;
+          done; done; true ;;
+    om4ab) for lib in $OM4LIBS; do
+             run c3test_$(basename $lib .so) 300 env BA_HIP_LIB=$ROOT/$lib python -u -m pytest tests/test_gpu.py tests/test_gpu_fullsize.py -m gpu -q -k "om4 or wave4 or config3 or depth4 or m4" --timeout 200 --timeout-method thread || exit $?
+           done
+           for rep in 1 2; do for lib in $OM4LIBS; do
+             echo "lib=$lib rep=$rep $(BA_HIP_LIB=$ROOT/$lib timeout -k 10 200 python tools/config3_prof.py --mode staged,inkernel --reps 10 2>/dev/null | grep '^{' | python3 -c 'import sys,json; print(" ".join("%s=%.4g" % (d["mode"], d["trials_per_s"]) for d in map(json.loads, sys.stdin)))')" >> gpurun_out/om4ab.log || exit $?
+           done; done ;;
     handoff) run pytest_handoff 300 python -u -m pytest tests/test_gpu_handoff.py -m gpu -v --timeout 120 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
     casc) run pytest_casc 600 python -u -m pytest tests/test_gpu_cascade.py tests/test_dist.py -m gpu -v --timeout 200 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
     c5prof) for b in 1024 1; do
