@@ -679,15 +679,24 @@ static bool co_admit(ba_ctx* ctx, hipStream_t s, uint64_t pollers) {
         if (c != ctx && c->device == ctx->device) busy += c->co_pending;
     if (busy + pollers <= budget) return true;
     busy = 0;
+    const bool trace = getenv("BA_TEST_CO_TRACE") != nullptr;  // tests: the admission's view
     for (ba_ctx* c : co_registry().ctxs) {
         if (c == ctx || c->device != ctx->device || c->co_pending == 0) continue;
         // a stream being captured may not be queried: its launches count
-        if (!stream_capturing(c->co_stream) && hipStreamQuery(c->co_stream) == hipSuccess) {
+        const bool cap = stream_capturing(c->co_stream);
+        const hipError_t q = cap ? hipErrorNotReady : hipStreamQuery(c->co_stream);
+        if (trace)
+            fprintf(stderr, "co_admit ctx %p: other ctx %p pending %llu stream %p query %d\n", (void*)ctx,
+                    (void*)c, (unsigned long long)c->co_pending, (void*)c->co_stream, (int)q);
+        if (q == hipSuccess) {
             c->co_pending = 0;
             continue;
         }
         busy += c->co_pending;
     }
+    if (trace)
+        fprintf(stderr, "co_admit ctx %p: busy %llu + %llu vs budget %llu\n", (void*)ctx,
+                (unsigned long long)busy, (unsigned long long)pollers, (unsigned long long)budget);
     return busy + pollers <= budget;
 }
 

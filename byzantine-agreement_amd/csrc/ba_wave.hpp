@@ -1133,6 +1133,11 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM4W_BLOCKS_PER_CU) void k_om4w(
                             lie3[e] = odd ? ov : ev;
                         });
                         lie2 = odd ? hi(l4) : rcv;
+                        if constexpr (!BA_OM4W_L1W) {  // lab A/B (bit 0 off): the round's own level-1 call
+                            uint64_t h0, h1;
+                            lie_pair(seed, 1, x1 >> 1, gw, h0, h1);
+                            lie1 = (x1 & 1u) ? h1 : h0;
+                        }
                     } else {
                         constexpr int NG = NPD + (BA_OM4W_L1W ? 1 : 2);
                         P4 pc[NG];

@@ -115,8 +115,10 @@ def test_handoff_timeout_multi_rank_job(engine, monkeypatch):
 
 
 def _stall_and_co(engines, B, stall_trials):
-    """On each engine's own stream: a long k_om3w call, then one CO-eligible
-    n=16, m=5 call of B instances (same inputs on every engine).  Returns the
+    """One CO-eligible n=16, m=5 call of B instances (same inputs) on each engine's
+    own stream, all held behind one gate: a long k_om3w call on a separate ctx's
+    stream, which every engine's stream waits for (an event), so that no CO call
+    can start -- or finish -- while the calls are being queued.  Returns the
     per-engine profiles and the decisions / outcomes / counters."""
     import torch
     from ba_amd import lib as L
@@ -125,32 +127,45 @@ def _stall_and_co(engines, B, stall_trials):
     sp = L.make_params(10, 3, 1, L.LIE_PHILOX, L.FAULTY_RANDOM, 3, L.ORDER_RANDOM, L.ATTACK, L.ENGINE_AUTO, 0)
     p = L.make_params(N, M, 0xC0AD, L.LIE_PHILOX, L.FAULTY_RANDOM, 5, L.ORDER_RANDOM, L.ATTACK,
                       L.ENGINE_LEVELS, 64 * 3)
-    scnt = torch.zeros((k, 16), dtype=torch.int64, device=dev)
+    scnt = torch.zeros(16, dtype=torch.int64, device=dev)
     dec = torch.empty((k, B), dtype=torch.int64, device=dev)
     out = torch.empty((k, B), dtype=torch.uint8, device=dev)
     cnt = torch.zeros((k, 16), dtype=torch.int64, device=dev)
     for i, e in enumerate(engines):  # warm-up: geometry, scratch, fan-in counters
-        e.run_device(sp, 4096, d_counters=scnt[i].data_ptr(), stream=e.stream())
         e.run_device(p, B, d_decisions=dec[i].data_ptr(), d_outcome=out[i].data_ptr(),
                      d_counters=cnt[i].data_ptr(), stream=e.stream())
         torch.cuda.synchronize()
-    # the admission counts another ctx's last CO launch until that ctx's stream
-    # is seen idle (co_admit, conservative): one more CO call on a scratch ctx
+    # the admission counts another ctx's last CO launch until a later admission
+    # sees that ctx's stream idle (co_admit, conservative: only the slow path
+    # queries, and a stream kept busy by other work keeps counting).  One more
+    # CO call on a scratch ctx with a one-launch budget takes the slow path,
     # sees every warm-up done, and closing that ctx drops its own launch
-    ew = L.Engine(0)
-    ew.run_device(p, B, d_counters=scnt[0].data_ptr(), stream=ew.stream())
-    torch.cuda.synchronize()
-    ew.close()
+    import os
+    os.environ["BA_TEST_CO_BUDGET"] = str(4 * 15)
+    try:
+        ew = L.Engine(0)
+        ew.run_device(p, B, d_counters=scnt.data_ptr(), stream=ew.stream())
+        torch.cuda.synchronize()
+        ew.close()
+    finally:
+        del os.environ["BA_TEST_CO_BUDGET"]
     cnt.zero_()
+    gate = L.Engine(0)  # never launches a CO cascade: counts nothing itself
+    gs = torch.cuda.ExternalStream(gate.stream(), device=dev)
     torch.cuda.synchronize()
-    for e in engines:
-        e.profile(True)
-    for i, e in enumerate(engines):
-        e.run_device(sp, stall_trials, d_counters=scnt[i].data_ptr(), stream=e.stream())
-    for i, e in enumerate(engines):
-        e.run_device(p, B, d_decisions=dec[i].data_ptr(), d_outcome=out[i].data_ptr(),
-                     d_counters=cnt[i].data_ptr(), stream=e.stream())
-    torch.cuda.synchronize()
+    try:
+        gate.run_device(sp, stall_trials, d_counters=scnt.data_ptr(), stream=gate.stream())
+        ev = torch.cuda.Event()
+        ev.record(gs)
+        for e in engines:
+            e.profile(True)
+            torch.cuda.ExternalStream(e.stream(), device=dev).wait_event(ev)
+        for i, e in enumerate(engines):
+            e.run_device(p, B, d_decisions=dec[i].data_ptr(), d_outcome=out[i].data_ptr(),
+                         d_counters=cnt[i].data_ptr(), stream=e.stream())
+        torch.cuda.synchronize()
+    finally:
+        gate.close()
     profs = [e.profile_read() for e in engines]
     for e in engines:
         e.profile(False)
