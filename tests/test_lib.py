@@ -170,3 +170,28 @@ def test_register_spill_budgets():
     bench = [r for n, r in res.items() if n.startswith("_ZN2ba6k_om3wILi10ELi0ELb1E")]
     assert len(bench) == 1 and bench[0]["vgpr_spill"] == 0 and bench[0]["vgpr"] <= 168, bench
     assert checked >= 60, checked
+
+
+def test_check_handoff_reads_slot14():
+    """ba_amd.lib.check_handoff: counter slot 14 (BA_C_HANDOFF_LOST, include/ba.h)
+    non-zero means a lost in-launch hand-off -> BAError(EDEVICE); zero passes, for
+    the counter containers the device-path callers hold (list, numpy, torch)."""
+    import numpy as np
+    import torch
+
+    from ba_amd import lib as L
+    hdr = open(os.path.join(ROOT, "include", "ba.h")).read()
+    assert re.search(r"#define BA_C_CHECK_MISMATCH 14\b", hdr)
+    assert re.search(r"#define BA_C_HANDOFF_LOST BA_C_CHECK_MISMATCH\b", hdr)
+    assert L.C_HANDOFF_LOST == 14
+    ok = [0] * 16
+    ok[0] = 64
+    for c in (ok, np.array(ok, np.int64), torch.tensor(ok, dtype=torch.int64),
+              dict(zip(L.COUNTER_NAMES, ok))):
+        L.check_handoff(c)
+    bad = list(ok)
+    bad[14] = 3
+    for c in (bad, np.array(bad, np.int64), torch.tensor(bad, dtype=torch.int64)):
+        with pytest.raises(L.BAError) as ei:
+            L.check_handoff(c)
+        assert ei.value.code == L.EDEVICE and "hand-off timed out" in str(ei.value)

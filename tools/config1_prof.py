@@ -48,6 +48,33 @@ def config1_inputs(n: int, T: int):
     return seeds, faulty, poll, order
 
 
+def mt_roofline(n: int, T: int, stride: int, sec: float) -> dict:
+    """HBM roofline of one k_mt_table launch over T trials lasting `sec`: the bytes
+    it must move (seed 8 B + faulty 4 B + poll 4 B read, 4 x stride B of coin row
+    written, per trial), with the committed same-build PMC's traffic and VALU
+    issue beside it (bench.pmc_for: matched by n, T, "mt_table" and the library's
+    sha256)."""
+    io = (8 + 4 + 4 + 4 * stride) * T
+    pmc, src, same = bench.pmc_for(n, 1, T, "mt_table", "k_mt_table", bench.so_digest())
+    traffic = pmc["traffic_bytes"] if pmc else None
+    roof = {"bound": "hbm", "kernel": "k_mt_table", "avg_ms": round(sec * 1e3, 4),
+            "achieved": round(io / sec / 1e9, 1), "peak": bench.HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(io / sec / 1e9 / bench.HBM_PEAK_GBS, 4),
+            "algorithmic_bytes_per_trial": io / T, "algorithmic_bytes_per_launch": io,
+            "traffic": round(traffic) if traffic else None,
+            "traffic_per_trial": round(traffic / T, 1) if traffic else None,
+            "traffic_GBps": round(traffic / sec / 1e9, 1) if traffic else None,
+            "source": src, "same_build": same,
+            "note": "the MT19937 state between random.seed and the draws is scratch (a window "
+                    "per wave, DESIGN.md section 4): traffic above the algorithmic bytes; the "
+                    "kernel is bound by the seeding recurrences (valu_frac)"}
+    if pmc and pmc.get("counters", {}).get("SQ_INSTS_VALU"):
+        insts = pmc["counters"]["SQ_INSTS_VALU"]
+        roof["valu_frac"] = round(insts * bench.VALU_ISSUE_CYCLES / (bench.SIMDS * sec * bench.CLOCK_GHZ * 1e9), 4)
+        roof["valu_insts_per_launch"] = insts
+    return roof
+
+
 def ev_time(fn, reps, stream):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
@@ -101,22 +128,7 @@ def main():
         raise SystemExit(f"config 1 n={n}: device coin table differs from the host replay")
     t_gen = ev_time(gen, a.reps, st)
     t_tab = ev_time(trials, a.reps, st)
-    io = (8 + 4 + 4 + 4 * stride) * T
-    digest = bench.so_digest()
-    pmc, src, same = bench.pmc_for(n, 1, T, "mt_table", "k_mt_table", digest)
-    traffic = pmc["traffic_bytes"] if pmc else None
-    roof = {"bound": "hbm", "kernel": "k_mt_table", "avg_ms": round(t_gen * 1e3, 4),
-            "achieved": round(io / t_gen / 1e9, 1), "peak": bench.HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(io / t_gen / 1e9 / bench.HBM_PEAK_GBS, 4),
-            "algorithmic_bytes_per_trial": io / T, "algorithmic_bytes_per_launch": io,
-            "traffic": round(traffic) if traffic else None,
-            "traffic_per_trial": round(traffic / T, 1) if traffic else None,
-            "traffic_GBps": round(traffic / t_gen / 1e9, 1) if traffic else None,
-            "source": src, "same_build": same}
-    if pmc and pmc.get("counters", {}).get("SQ_INSTS_VALU"):
-        insts = pmc["counters"]["SQ_INSTS_VALU"]
-        roof["valu_frac"] = round(insts * bench.VALU_ISSUE_CYCLES / (bench.SIMDS * t_gen * bench.CLOCK_GHZ * 1e9), 4)
-        roof["valu_insts_per_launch"] = insts
+    roof = mt_roofline(n, T, stride, t_gen)
     print(json.dumps({"what": "config1", "n": n, "trials": T, "table_stride": stride,
                       "device_table_ms": round(t_gen * 1e3, 4), "k_table_ms": round(t_tab * 1e3, 4),
                       "device_table_trials_per_s": T / t_gen,

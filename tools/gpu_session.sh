@@ -78,17 +78,18 @@ for s in $STAGES; do
           echo "c1prof $nn rc=$rc" | tee -a gpurun_out/steps.log; [ $rc -eq 0 ] || exit $rc; done ;;
     c1pmc) for nn in 4 10; do
          C1="$ROOT/tools/config1_prof.py --n $nn --reps 3"
+         # C1PMC_TAG / BA_HIP_LIB (optional): the same passes over a lab library (round-5 kernel)
          for pass in "sq:SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
                      "lds:SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
                      "fetch:FETCH_SIZE GRBM_GUI_ACTIVE GRBM_COUNT" "write:WRITE_SIZE"; do
            name=${pass%%:*}; ctrs=${pass#*:}
            (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $ctrs --output-format csv \
-              -d "$ROOT/gpurun_out/c1pmc_$nn" -o "$name" -- python3 $C1 > "$ROOT/gpurun_out/c1pmc_${nn}_$name.log" 2>&1)
+              -d "$ROOT/gpurun_out/c1pmc${C1PMC_TAG:-}_$nn" -o "$name" -- python3 $C1 > "$ROOT/gpurun_out/c1pmc${C1PMC_TAG:-}_${nn}_$name.log" 2>&1)
            rc=$?; echo "c1pmc $nn $name rc=$rc" | tee -a gpurun_out/steps.log; [ $rc -eq 0 ] || exit $rc
          done
-         python3 tools/pmc_summary.py gpurun_out/c1pmc_$nn gpurun_out/c1pmc_${nn}_summary.json \
+         python3 tools/pmc_summary.py gpurun_out/c1pmc${C1PMC_TAG:-}_$nn gpurun_out/c1pmc${C1PMC_TAG:-}_${nn}_summary.json \
            --workload "tools/config1_prof.py --n $nn: ba.py-exact OM(1), 1048576 trials" \
-           --config $nn,1,1048576,mt_table,k_mt_table > gpurun_out/c1pmc_${nn}_summary.log 2>&1
+           --config $nn,1,1048576,mt_table${C1PMC_TAG:-},k_mt_table > gpurun_out/c1pmc${C1PMC_TAG:-}_${nn}_summary.log 2>&1
        done ;;
     c1var) for lib in $C1LIBS; do
              run mttest_$(basename $lib .so) 200 env BA_HIP_LIB=$ROOT/$lib python -u -m pytest tests/test_gpu_mt.py -m gpu -q --timeout 100 --timeout-method thread || exit $?

@@ -24,7 +24,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "byzantine-agreement_amd", "ba_amd", "libba_hip.so")
+LIB = os.environ.get("BA_HIP_LIB") or os.path.join(ROOT, "byzantine-agreement_amd", "ba_amd", "libba_hip.so")
 
 SIMDS = 256 * 4
 

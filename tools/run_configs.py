@@ -174,6 +174,8 @@ def main():
             ms_both = e0.elapsed_time(e1) / 5
             if any(v != first[c] * 5 for c, v in counters(cnt).items()):
                 raise SystemExit("config 1: device-table runs disagree")
+            import config1_prof
+            mt_roof = config1_prof.mt_roofline(n, T, tab.shape[1], ms_gen * 1e-3)
             out.append({"config": 1, "workload": f"ba.py OM(1) bit-exact, n={n}, {T} trials, one "
                         "MT19937 seed per trial (random.seed + the round's coins in ba.py's draw "
                         "order), random faulty sets / stale-primary polls / orders",
@@ -192,7 +194,7 @@ def main():
                         "device_end_to_end_note": "ba_mt_table_device + k_table back to back on "
                                                   "one stream (seeds, faulty sets, polls, orders in "
                                                   "HBM; HIP events), table equal to the host's",
-                        "n_gpus": 1, "counters": first})
+                        "n_gpus": 1, "counters": first, "roofline": mt_roof})
             del d_tab, d_tab2, d_seeds, d_f, d_p, d_o, dec, outc
 
     if 3 in which:
