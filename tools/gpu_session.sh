@@ -63,6 +63,7 @@ for s in $STAGES; do
              cat gpurun_out/sched_$m.log >> gpurun_out/sched_all.jsonl
            done ;;
     configs) run configs 600 python -u tools/run_configs.py || exit $? ;;
+    configs1) run configs1 600 python -u tools/run_configs.py --only 1,3,4,5 || exit $? ;;
     c5) run c5_1024 300 python -u tools/config5_prof.py --batch 1024 --split || exit $?
         run c5_1 300 python -u tools/config5_prof.py --batch 1 --reps 500 --split || exit $? ;;
     multirank) run pytest_multirank 900 python -u -m pytest tests/test_multirank_gpu.py tests/test_dist.py -m gpu -v --timeout 420 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
@@ -113,6 +114,10 @@ for s in $STAGES; do
            for rep in 1 2; do for lib in $OM4LIBS; do
              echo "lib=$lib rep=$rep $(BA_HIP_LIB=$ROOT/$lib timeout -k 10 200 python tools/config3_prof.py --mode staged,inkernel --reps 10 2>/dev/null | grep '^{' | python3 -c 'import sys,json; print(" ".join("%s=%.4g" % (d["mode"], d["trials_per_s"]) for d in map(json.loads, sys.stdin)))')" >> gpurun_out/om4ab.log || exit $?
            done; done ;;
+    mcab) for rep in 1 2; do for lib in $MCLIBS; do
+            echo "lib=$lib rep=$rep" >> gpurun_out/mcab.log
+            BA_HIP_LIB=$ROOT/$lib timeout -k 10 200 python tools/run_configs.py --only 5 2>/dev/null | grep '^{' >> gpurun_out/mcab.log || exit $?
+          done; done ;;
     handoff) run pytest_handoff 300 python -u -m pytest tests/test_gpu_handoff.py -m gpu -v --timeout 120 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
     casc) run pytest_casc 600 python -u -m pytest tests/test_gpu_cascade.py tests/test_dist.py -m gpu -v --timeout 200 --timeout-method thread; rc=$?; fatal $rc && exit $rc ;;
     c5prof) for b in 1024 1; do
