@@ -189,3 +189,34 @@ def test_clock_from_probes_pairs_rows_by_cu():
     med, per = bench.clock_from_probes(p0, p1)
     assert per == {0: 2400.0, 1: 2300.0}
     assert med == 2350.0
+
+
+def test_lds_bank_model_matches_the_ablation_pmc():
+    """tools/lds_bank_model.py's per-task prediction for k_om3w<10> is what the
+    ablation builds measured (profiles/r06c_bank/: dropping the R2T leaf stores
+    removed 589,824 conflict cycles per 2,048-task launch, dropping the R1T
+    store 73,728 -- exactly 288 and 36 per task)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import lds_bank_model as M
+    m = M.model(10)
+    assert m["r2t_stores"] == 288 and m["r1t_stores"] == 36
+    assert m["r2t_columns"] == 0 and m["r1t_roots"] == 0 and m["e_gathers"] == 0
+    pmc = {}
+    for name in ("base", "nor2t", "nor1t"):
+        d = json.load(open(os.path.join(ROOT, "profiles", "r06c_bank", f"bank_om3_{name}_summary.json")))
+        (e,) = [v for k, v in d["kernels"].items() if "k_om3w<10, 0, true>" in k]
+        pmc[name] = e["counters"]["SQ_LDS_BANK_CONFLICT"]
+    assert pmc["base"] - pmc["nor2t"] == m["r2t_stores"] * 2048
+    assert pmc["base"] - pmc["nor1t"] == m["r1t_stores"] * 2048
+
+
+def test_config3_rooflines_from_committed_pmc():
+    """tools/config3_prof.rooflines finds the committed same-build-keyed PMC of
+    k_om4w<13> at 8M trials (profiles/r06j_pmc_om4w_*.json) and prices the three
+    rooflines; the HBM one is on the 14 B/trial of per-trial I/O."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import config3_prof as C
+    roof, valu, comp = C.rooflines(13, 4, 8 << 20, 10e-3, True, engine="auto/staged")
+    assert roof["algorithmic_bytes_per_trial"] == 14.0 and roof["traffic"] > 0
+    assert valu and valu["valu_insts_per_launch"] > 0
+    assert comp["calls_per_launch"] == 54192 * (8 << 20) // 64
