@@ -624,28 +624,37 @@ __global__ __launch_bounds__(kBlock) void k_table(uint32_t n, uint32_t relay, ui
         fm &= all;
         const uint32_t ob = oc == 1;
         const uint32_t* row = table + i * stride;
+        // the coin stream: coin c is bit c & 31 of row[c >> 5].  take(k) = the next
+        // k <= 31 coins as bits 0..k-1 (a word or two, not one load per coin)
         uint32_t c = 0;
-        auto coin = [&]() -> uint32_t {
-            const uint32_t v = (row[c >> 5] >> (c & 31)) & 1u;
-            ++c;
-            return v;
+        auto take = [&](uint32_t k) -> uint32_t {
+            if (k == 0) return 0u;
+            const uint32_t w = c >> 5, sh = c & 31u;
+            uint32_t v = row[w] >> sh;
+            if (sh + k > 32u) v |= row[w + 1] << (32u - sh);  // coins c..c+k-1 exist
+            c += k;
+            return v & ((1u << k) - 1u);
         };
-        uint32_t V = 0;
-        for (uint32_t r = 1; r < n; ++r) V |= ((fm & 1u) ? coin() : ob) << r;  // ba.py:263-277
+        const uint32_t cf = fm & 1u, lts = all & ~1u;
+        // ba.py:263-277: lieutenant r gets coin r-1 from a faulty commander
+        const uint32_t V = cf ? take(n - 1) << 1 : (ob ? lts : 0u);
         const uint32_t pm = poll ? poll[i] & all & ~1u : 0u;
+        // ba.py:159-195, receiver-major: receiver r counts V_r, the commander's
+        // answer to a stale poll, then every other lieutenant j ascending -- a coin
+        // from a faulty j, V_j from a loyal one.  Only the counts matter, so the
+        // loyal relays are one popcount and the faulty ones the popcount of their
+        // run of coins (the stream order is unchanged).
+        const uint32_t nfl = __popc(fm & lts), loyalV = V & ~fm & lts;
         uint32_t A = 0, U = 0;
-        for (uint32_t r = 1; r < n; ++r) {  // ba.py:159-195, receiver-major
+        for (uint32_t r = 1; r < n; ++r) {
             uint32_t a = (V >> r) & 1u, cnt = 1;
             if (relay) {
                 if ((pm >> r) & 1u) {  // stale primary_port: the commander answers too
-                    a += (fm & 1u) ? coin() : ob;
+                    a += cf ? take(1) : ob;
                     ++cnt;
                 }
-                for (uint32_t j = 1; j < n; ++j) {
-                    if (j == r) continue;
-                    a += ((fm >> j) & 1u) ? coin() : ((V >> j) & 1u);
-                    ++cnt;
-                }
+                a += __popc(loyalV & ~(1u << r)) + __popc(take(nfl - ((fm >> r) & 1u)));
+                cnt += n - 2;
             }
             if (2 * a > cnt) A |= 1u << r;
             else if (2 * a == cnt) U |= 1u << r;
