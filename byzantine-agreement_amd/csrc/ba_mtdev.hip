@@ -37,6 +37,9 @@ constexpr int kMtN = 624, kMtM = 397;
 #ifndef BA_MT_TPL
 #define BA_MT_TPL 2
 #endif
+#ifndef BA_MT_SORT
+#define BA_MT_SORT 1  // 0: lab A/B, trials in index order over the waves
+#endif
 #ifndef BA_MT_STREAM
 #define BA_MT_STREAM 1  // 0: lab A/B, every window drawn after the sweep (mt_draw)
 #endif
@@ -75,15 +78,15 @@ __device__ __forceinline__ uint32_t om1_coins(uint32_t n, uint32_t m, uint32_t f
     return c;
 }
 
-// Draw the round's coins (and the next word) from the state stored at the
-// slots `slot(i)` maps state positions to, twisting lazily in place: output k
+// Draw the round's coins (and the next word) of trial t from the state stored
+// in column `col` (rows of T words) at the slots `slot(i)` maps state positions to, twisting lazily in place: output k
 // reads positions k, k+1 and k+397 (mod 624; a position below k+397-624 is
 // already new, as in CPython's in-place twist).  `lim` = the number of outputs
 // the stored positions allow (a window), or 0 for the full state (any number,
 // second twists included: positions wrap).  Returns false if the lane needed
 // more than `lim` outputs (it then starts over on the full state).
 template <typename Slot>
-__device__ __forceinline__ bool mt_draw(uint32_t* __restrict__ st, uint64_t T, uint64_t t, Slot slot,
+__device__ __forceinline__ bool mt_draw(uint32_t* __restrict__ col, uint64_t T, uint64_t t, Slot slot,
                                         uint32_t lim, uint32_t cnt, bool want_next, uint32_t* row,
                                         uint32_t* __restrict__ next_word) {
     constexpr uint32_t kBlk = kMtDrawBlk;
@@ -98,7 +101,6 @@ __device__ __forceinline__ bool mt_draw(uint32_t* __restrict__ st, uint64_t T, u
             // every lane still drawing is at the same position: row addresses
             // are wave-uniform (scalar), the lane's column its offset
             const uint32_t upos = (uint32_t)__builtin_amdgcn_readfirstlane((int)pos);
-            uint32_t* col = st + t;
             auto at = [&](uint32_t i) { return col + (uint64_t)slot(i) * T; };
             uint32_t cur[kBlk + 1], far[kBlk];
             static_for<0, kBlk + 1>([&](auto k) {
@@ -354,14 +356,19 @@ __device__ __forceinline__ void mt_stream_range(uint32_t i0, uint32_t i1, uint32
     auto draw = [&](uint32_t k, const uint32_t (&nx)[J]) {
         static_for<0, J>([&](auto j) { mt_stream_out(S[j()], c2[j()], nx[j()], k, row[j()]); });
     };
+    auto load4 = [&](uint32_t k, uint32_t (&nx)[4][J]) {
+        static_for<0, 4>([&](auto q) {
+            static_for<0, J>([&](auto j) { nx[q()][j()] = col[j()][(uint64_t)(k + 1 + q()) * R]; });
+        });
+    };
     uint32_t i = i0;
+    // (loading the next group's words a group ahead measured 3-8% slower: 112
+    // VGPRs, r06v)
     for (; i + 4 <= i1; i += 4) {
         const uint32_t k = i - (uint32_t)kMtM;
         if (need()) {
             uint32_t nx[4][J];
-            static_for<0, 4>([&](auto q) {
-                static_for<0, J>([&](auto j) { nx[q()][j()] = col[j()][(uint64_t)(k + 1 + q()) * R]; });
-            });
+            load4(k, nx);
             mt_mix_one<J, false, false>(kMtInit.v[i], i, c1, c2, add_even, add_odd, nop, R);
             draw(k, nx[0]);
             mt_mix_one<J, false, true>(kMtInit.v[i + 1], i + 1, c1, c2, add_even, add_odd, nop, R);
@@ -499,12 +506,56 @@ __global__ __launch_bounds__(kMtBlock) void k_mt_table(uint32_t n, uint32_t m, u
     uint32_t cnt[J], need = 0;
     bool live[J];
     uint32_t* col[J];
+    const uint64_t base = (uint64_t)blockIdx.x * (kMtBlock * J);
+    if constexpr (BA_MT_SORT) {
+        // The block's trials go to its waves in order of coin count (a bitonic
+        // sort of (cnt, index) keys in LDS): a wave's window -- its largest trial's
+        // -- then fits its trials, where in index order nearly every wave held
+        // a trial near the block's largest count, and a wave of trials that draw
+        // nothing skips random.seed altogether (n=4: 0.26 -> 0.21 ms per 1M
+        // trials; n=10 the same).  Trial t_j's scratch column is its sorted
+        // position (the wave's stores stay one 256-B segment).
+        constexpr uint32_t NK = kMtBlock * J;
+        __shared__ uint32_t key[NK];
+        static_for<0, J>([&](auto j) {
+            const uint32_t li = j() * kMtBlock + threadIdx.x;
+            const uint64_t tt = base + li;
+            const uint32_t c = tt < T ? om1_coins(n, m, faulty[tt], poll ? poll[tt] : 0u) : 0u;
+            key[li] = c << 10 | li;  // c < 2^22 (n <= 32)
+        });
+        __syncthreads();
+        for (uint32_t k = 2; k <= NK; k <<= 1) {
+            for (uint32_t h = k >> 1; h > 0; h >>= 1) {
+                for (uint32_t q = threadIdx.x; q < NK / 2; q += kMtBlock) {
+                    const uint32_t i = 2 * h * (q / h) + q % h;
+                    const uint32_t a = key[i], b = key[i + h];
+                    if ((a > b) == ((i & k) == 0)) {
+                        key[i] = b;
+                        key[i + h] = a;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        // (wave w taking sorted quarter (w + block) mod 4 instead measured the same)
+        const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+        static_for<0, J>([&](auto j) {
+            const uint32_t p = wave * (64u * J) + j() * 64u + lane, kk = key[p];
+            t[j()] = base + (kk & 1023u);
+            cnt[j()] = kk >> 10;
+            col[j()] = st + base + p;
+        });
+    } else {
+        static_for<0, J>([&](auto j) {
+            t[j()] = base + j() * kMtBlock + threadIdx.x;
+            cnt[j()] = t[j()] < T ? om1_coins(n, m, faulty[t[j()]], poll ? poll[t[j()]] : 0u) : 0u;
+            col[j()] = st + t[j()];
+        });
+    }
     static_for<0, J>([&](auto j) {
-        t[j()] = (uint64_t)blockIdx.x * (kMtBlock * J) + j() * kMtBlock + threadIdx.x;
         live[j()] = t[j()] < T;
-        cnt[j()] = live[j()] ? om1_coins(n, m, faulty[t[j()]], poll ? poll[t[j()]] : 0u) : 0u;
         seed[j()] = live[j()] ? seeds[t[j()]] : 0ull;
-        col[j()] = st + t[j()];  // t < R: padding columns for the dead trials
+        // (columns < R: padding columns for the dead trials)
         // the outputs this trial's window holds (whole draw blocks)
         const uint32_t nj = live[j()] && (cnt[j()] != 0 || want_next)
                                 ? 2u * cnt[j()] + cnt[j()] / 2u + 16u + (want_next ? 1u : 0u) : 0u;
@@ -541,7 +592,7 @@ __global__ __launch_bounds__(kMtBlock) void k_mt_table(uint32_t n, uint32_t m, u
         auto slot = [wv](uint32_t i) { return i <= wv ? i : wv + 1u + (i - (uint32_t)kMtM); };
         static_for<0, J>([&](auto j) {
             if (live[j()])
-                ok[j()] = mt_draw(st, R, t[j()], slot, wv, cnt[j()], want_next, table + t[j()] * stride,
+                ok[j()] = mt_draw(col[j()], R, t[j()], slot, wv, cnt[j()], want_next, table + t[j()] * stride,
                                   next_word);
         });
     } else {
@@ -554,7 +605,8 @@ __global__ __launch_bounds__(kMtBlock) void k_mt_table(uint32_t n, uint32_t m, u
             uint32_t* const c1[1] = {col[j()]};
             const uint64_t s1[1] = {seed[j()]};
             mt_seed<1>(c1, R, s1, (uint32_t)kMtN, 0u);
-            (void)mt_draw(st, R, t[j()], [](uint32_t i) { return i; }, 0u, cnt[j()], want_next, row, next_word);
+            (void)mt_draw(col[j()], R, t[j()], [](uint32_t i) { return i; }, 0u, cnt[j()], want_next, row,
+                          next_word);
         }
         for (uint32_t wi = (cnt[j()] + 31) >> 5; wi < stride; ++wi) row[wi] = 0;  // the row's unused words
     });
