@@ -898,9 +898,11 @@ __global__ __launch_bounds__(kWaveThreads, BA_OM3W_MIN_BLOCKS(N)) void k_om3w(
         // ---- subtree rounds ------------------------------------------------------
         const uint64_t gw = gw0 + lw;
         for (uint32_t j1 = 0; j1 < (uint32_t)L; ++j1) {
-            // lab only: alternate the issue priority of the SIMD's two waves every
-            // round (round 1 default; round 2 measured it 2.5 us slower, om3_lab)
-            if constexpr ((DIAG & 8) != 0) wave_alternate_priority(j1);
+            // the issue priority of the SIMD's two waves alternates every round
+            // (round 6: a one-stream launch 50.0 -> 48.8 us, two steps in flight the
+            // same, profiles/r06za_om3w_prio_ab.log; round 2's kernel had measured
+            // it 2.5 us slower).  DIAG & 8: lab, without
+            if constexpr ((DIAG & 8) == 0) wave_alternate_priority(j1);
             const uint64_t r1 = om3_round<N, true>(in, act ? img[G::oL0 + lw * L + j1] : 0ull,
                                                    img + G::oR2, lw, la, act, j1, seed, gw,
                                                    erow, &lofs);

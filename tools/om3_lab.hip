@@ -398,7 +398,7 @@ static int compare_wave(uint64_t B) {
     printf("{\"wave_lds56k_us\": %.2f}\n", vpad);
     const float vprio = time_launch(k_om3w<10, 8>, gridw, ldsw, 0xBA5EEDull, gs, 0ull, B,
                                   (const uint32_t*)nullptr, (const uint8_t*)nullptr, d2, o2, c2, g_sink);
-    printf("{\"wave_prio_alternating_us\": %.2f}\n", vprio);
+    printf("{\"wave_prio_fixed_us\": %.2f}\n", vprio);  // DIAG 8: without the alternation
     {
         uint32_t* sf;
         uint8_t* so;
