@@ -212,7 +212,7 @@ def test_lds_bank_model_matches_the_ablation_pmc():
 
 def test_config3_rooflines_from_committed_pmc():
     """tools/config3_prof.rooflines finds the committed same-build-keyed PMC of
-    k_om4w<13> at 8M trials (profiles/r06x_pmc_om4w_*.json) and prices the three
+    k_om4w<13> at 8M trials (profiles/r06zb_pmc_om4w_*.json) and prices the three
     rooflines; the HBM one is on the 14 B/trial of per-trial I/O."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import config3_prof as C
